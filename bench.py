@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: path_trace_pixel -> ray_query BVH traversal ->
+tonemap_pixel under baseline_render, on MI355X.
+
+Workload (BASELINE.json configs[1]): frame 0 of the reference animation,
+1280x720, 256 samples per pixel, MAX_BOUNCES = 4 (the shipped TESTING
+preset), the reference scene (reference OBJ assets + committed substitutes for
+the three missing meshes).  One step = what the reference does per frame
+after load_scene: setup_animation_frame (host C++) + upload of the frame's
+TLAS/instances/subframes + the full-frame render on the GPU (+ the RCCL
+framebuffer gather in --shard tiles mode), inputs of the static scene already
+resident in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run).  --shard frames
+(default): rank r renders frame (frame + r) - weak scaling, no collective on
+the data path (BASELINE config 4 style).  --shard tiles: one frame split into
+interleaved 32x16 tiles, rank 0 gathers the BGRA tiles over RCCL and
+assembles the framebuffer - strong scaling (config 3 style).
+
+Prints ONE JSON line (rank 0) with the driver contract fields plus
+"roofline" (k_trace: algorithmic bytes / device time from HIP events, vs
+8 TB/s HBM) and "cpu_baseline" (the reference's own baseline_render built
+from its sources, timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(c):
+    """B = 32 N_node + 60 N_tri + 88 N_enter + 156 N_hit + 160 per sample.
+
+    32 B TravRec per node visit (24 B box + 8 B link in the reference layout),
+    60 B per triangle test (3 x u32 index + 3 x 16 B position), 88 B per BLAS
+    entry (blas + mesh + inv_transform), 156 B per closest-hit shade (3 x u32 +
+    9 x 16 B vertex attributes), 160 B subframe per sample."""
+    samples, visits, tris, enters, queries, shades = [int(x) for x in c[:6]]
+    return 32 * visits + 60 * tris + 88 * enters + 156 * shades + 160 * samples
+
+
+def cpu_baseline(assets, frame):
+    """Reference baseline_render (main.cc:12) on this host, bounded sample."""
+    from oracle import Reference
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    ref = Reference("v3", 1280, 720, 16, 4)
+    if not ref.available():
+        return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference",
+                "sample": "unavailable: %s not built" % ref.exe}
+    r = ref.baseline(assets, frame, threads=threads, timeout=900)
+    return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": r["threads"], "kind": "reference",
+            "sample": "frame %d, 1280x720 x 16 spp (%.1f M samples, full frame) through the reference's own "
+                      "baseline_render (main.cc:12-46, OpenMP static schedule) built from /root/reference sources "
+                      "with the reference flags (-O3 -ffast-math, -march=x86-64-v3); render %.2f s"
+                      % (frame, 1280 * 720 * 16 / 1e6, r["render_s"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frame", type=int, default=0)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--shard", choices=["frames", "tiles"], default="frames")
+    ap.add_argument("--tile", type=str, default="32x16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ptlumi_loader  # noqa: F401
+    from ptlumi import native as N
+    from ptlumi.renderer import GpuRenderer
+    from ptlumi import distributed as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    assets = os.path.join(ROOT, "assets")
+    cfg = N.RenderConfig.make(args.width, args.height, args.spp, args.bounces)
+    scene = N.Scene(assets, cfg)
+    r = GpuRenderer(local)
+    stream = torch.cuda.current_stream(local)
+    r.set_stream(stream)
+    tw, th = [int(v) for v in args.tile.split("x")]
+    frame = args.frame + (rank if args.shard == "frames" else 0)
+
+    # static scene once (load_scene output) - resident in HBM before timing
+    scene.setup_frame(frame)
+    r.upload(scene, include_static=True)
+    dev = torch.device("cuda", local)
+    image = torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device=dev)
+    shard = D.TileShard(cfg, tw, th, rank, world) if args.shard == "tiles" else None
+
+    def step():
+        scene.setup_frame(frame)                     # setup_animation_frame (host)
+        r.upload(scene, include_static=False)        # per-frame TLAS/instances/subframes
+        if shard is None:
+            r.render(cfg, out_bgra=image)
+        else:
+            D.render_and_gather(r, cfg, shard, image, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(local)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    r.enable_timing(True)
+    trace_ms, trace_launches = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        ms, n = r.last_timing()       # waits for this step's k_trace launches
+        trace_ms += ms
+        trace_launches += n
+    torch.cuda.synchronize(local)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    elapsed = time.perf_counter() - t0
+    r.enable_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    result = None
+    if rank == 0:
+        roof = None
+        if not args.no_roofline:
+            # deterministic work counters of the same render (separate counting pass, untimed)
+            r.enable_counters(True)
+            if shard is None:
+                r.render(cfg, out_bgra=image)
+            else:
+                r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+            r.synchronize()
+            c = r.counters()
+            r.enable_counters(False)
+            per_step_samples = int(c[0])
+            alg = algorithmic_bytes(c)
+            launches_per_step = trace_launches / args.steps
+            ms_per_launch = trace_ms / trace_launches
+            bytes_per_launch = alg / launches_per_step
+            achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "k_trace", "ms_per_launch": round(ms_per_launch, 3),
+                    "launches_per_step": launches_per_step,
+                    "algorithmic_bytes_per_sample": round(alg / per_step_samples, 1),
+                    "per_sample": {"node_visits": round(c[1] / per_step_samples, 2),
+                                   "triangle_tests": round(c[2] / per_step_samples, 2),
+                                   "blas_entries": round(c[3] / per_step_samples, 2),
+                                   "ray_queries": round(c[4] / per_step_samples, 3),
+                                   "shades": round(c[5] / per_step_samples, 3)}}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(assets, args.frame)
+            except Exception as e:  # reported, never fatal to the GPU measurement
+                cpu = {"value": None, "unit": "Msamples/s", "cores": None, "kind": "reference",
+                       "sample": "failed: %s" % str(e)[:300]}
+        result = {
+            "metric": "Msamples/sec (whole node) at 1280x720 256spp, frame 0",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak" if args.shard == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference scene assets + deterministic substitutes, frame %d" % args.frame,
+            "config": {"workload": "frame %d, %dx%d, %d spp, %d bounces (BASELINE configs[1])"
+                                   % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel, cfg.max_bounces),
+                       "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu and cpu.get("value"):
+            result["gpu_vs_cpu"] = round(value / cpu["value"], 2)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    r.close()
+    return result
+
+
+if __name__ == "__main__":
+    main()

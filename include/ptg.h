@@ -223,11 +223,20 @@ int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4*
  * (path_tracer.hh:415-427).  HOST pointers; synchronous. */
 int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* rays, uint32_t* hits);
 
-/* Work counters of the last ptg_render* call (filled only when the
- * environment variable PTG_COUNTERS=1 was set at context creation):
+/* Work counters of the last ptg_render* call (filled only while counting is
+ * on: ptg_counters_enable, or PTG_COUNTERS=1 at context creation; counting
+ * uses a separate, slower build of the kernel):
  * [0] samples, [1] node visits, [2] triangle tests, [3] BLAS entries,
  * [4] ray queries, [5] closest-hit shades. */
+int ptg_counters_enable(ptg_context* ctx, int enable);
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
+
+/* Per-launch timing of the path-tracing kernel (k_trace), measured with HIP
+ * events on the context's stream.  After enabling, each ptg_render* call
+ * records its launches; ptg_last_timing returns their summed device time and
+ * count (waits for the last launch). */
+int ptg_timing_enable(ptg_context* ctx, int enable);
+int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches);
 
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);

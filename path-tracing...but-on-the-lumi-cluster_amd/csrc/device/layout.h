@@ -1,0 +1,79 @@
+// Device-side data layout in HBM (shared by the HIP kernels and the host
+// code that packs it).  See DESIGN.md "Data layout in HBM".
+//
+// The reference arrays (bvh_node 24 B + 8 link orders of 8 B, indices +
+// float3 positions) are repacked once on the GPU into records that a
+// traversal step reads with one or two 16-byte loads:
+//   TravRec   32 B  one (node, octant) pair: AABB + that octant's link.
+//                   trav[node_offset*8 + octant*node_count + i] - the same
+//                   index the reference uses for links[] (ray_query.hh:139-140),
+//                   so the link offset arithmetic carries over unchanged.
+//   TriRec    48 B  the three vertex positions of triangle t of a mesh,
+//                   tris[index_offset/3 + t] (ray_query.hh:228-234 gathers
+//                   indices then positions: two dependent loads -> one).
+//   InstTrav  64 B  what ray_query_enter_blas needs (ray_query.hh:153-182):
+//                   inv_transform columns xyz of rows 0..3, BLAS handle and
+//                   the mesh's triangle base.
+//   InstShade 64 B  what the closest-hit shading needs (path_tracer.hh:369-392):
+//                   transform rows 0..2 xyz and the mesh offsets.
+// BLAS records live in one buffer (uploaded once); the per-frame TLAS
+// records live in a second buffer, indexed from the first frame node.
+#pragma once
+#include <stdint.h>
+
+namespace ptg {
+
+struct alignas(16) TravRec {
+    float min_x, min_y, min_z;
+    uint32_t accept;           // top bit: leaf; payload in the low 31 bits
+    float max_x, max_y, max_z;
+    uint32_t cancel;           // next node when the box is missed / after a leaf
+};
+static_assert(sizeof(TravRec) == 32, "TravRec is two 16-byte loads");
+
+struct alignas(16) TriRec {
+    float p0x, p0y, p0z, p1x;
+    float p1y, p1z, p2x, p2y;
+    float p2z, pad0, pad1, pad2;
+};
+static_assert(sizeof(TriRec) == 48, "TriRec is three 16-byte loads");
+
+struct alignas(16) InstTrav {
+    float m[12];               // inv_transform.r[k].{x,y,z} for k = 0..3
+    uint32_t blas_count, blas_offset, tri_base, pad;
+};
+static_assert(sizeof(InstTrav) == 64, "InstTrav is four 16-byte loads");
+
+struct alignas(16) InstShade {
+    float rot[9];              // transform.r[k].{x,y,z} for k = 0..2
+    uint32_t index_offset, base_vertex_offset, pad[5];
+};
+static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
+
+// Everything a hot-path kernel reads, passed by value as a kernel argument.
+struct DevScene {
+    const TravRec* blas_trav;      // static BVH records (BLAS), index = global link index
+    const TravRec* tlas_trav;      // per-frame TLAS records, index = global link index - 8*first_frame_node
+    const TriRec* tris;
+    const InstTrav* inst_trav;
+    const InstShade* inst_shade;
+    const uint32_t* indices;
+    const float* normal;           // reference float3[] (16 B stride)
+    const float* albedo;           // float4[]
+    const float* material;         // float4[]
+    const uint8_t* subframes;      // reference subframe[] (160 B each)
+    uint32_t tlas_link_base;       // 8 * first_frame_node
+    uint32_t width, height, spp, max_bounces, student_id, blur_step;
+    uint32_t subframe_count;
+};
+
+// Reference subframe byte offsets (scene.hh:26-34, verified in include/ptg.h users)
+enum : uint32_t {
+    SF_STRIDE = 160,
+    SF_TLAS = 0,                  // bvh {node_count, node_offset}
+    SF_CAM = 16,                  // camera: orientation rows @0,16,32; position @48; aspect @64,
+                                  //   inv_focal @68, focal_dist @72, ap_angle @76, ap_polygon @80, ap_radius @84
+    SF_LIGHT = 112,               // light: direction @0, color @16, cos_solid_angle @32
+};
+
+} // namespace ptg

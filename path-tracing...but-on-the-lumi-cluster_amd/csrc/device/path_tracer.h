@@ -1,0 +1,680 @@
+// Device path tracer: the reference hot path re-expressed for gfx950.
+//
+//   trace()              two-level stackless BVH walk with the reference's
+//                        link order (ray_query.hh:111-290) as ONE flat loop:
+//                        TLAS and BLAS steps, BLAS entry and triangle tests
+//                        are all iterations of the same loop, so lanes of a
+//                        wave that sit in different levels still step
+//                        together (no nested per-level loops to diverge in).
+//   path_trace_sample()  path_trace_pixel (path_tracer.hh:637-741).
+//   tonemap()            tonemap_pixel (path_tracer.hh:753-771).
+//
+// Results are bit-identical to the reference's C++ evaluated in IEEE
+// arithmetic (oracle/pt_oracle.c): every float/double expression below keeps
+// the reference's operand order and precision; see ref_math.h for the rules.
+#pragma once
+#include "layout.h"
+#include "ref_math.h"
+
+namespace ptg {
+namespace dm {
+
+constexpr float EARTH_RADIUS = 6.3781e6f;
+constexpr float ATMOSPHERE_HEIGHT = 1.0e5f;
+constexpr float RAYLEIGH_SCALE_HEIGHT = 7994.0f;
+constexpr float MIE_SCALE_HEIGHT = 1200.0f;
+constexpr float MIE_ANISOTROPY = 0.80f;
+constexpr float MIN_RAY_DIST = 1e-4f;
+constexpr float MAX_RAY_DIST = 1e9f;
+constexpr float REGULARIZATION_GAMMA = 0.15f;
+constexpr int PRIMARY_ITERATIONS = 8;
+constexpr int SECONDARY_ITERATIONS = 4;
+
+// Work counters (only in the counting build of a kernel).
+struct Counters {
+    uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0;
+};
+
+struct Hit {
+    float bx, by, bz, thit;
+    uint32_t instance_id, primitive_id;
+    bool back_face;
+};
+
+PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : 1.0f / d; }   // 1/d, 0 -> (float)1e40
+PTG_D uint32_t octant(f3 d) { return (d.x > 0 ? 1u : 0u) | (d.y > 0 ? 2u : 0u) | (d.z > 0 ? 4u : 0u); }
+
+PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
+{
+    const float4* q = reinterpret_cast<const float4*>(p);
+    lo = q[0];
+    hi = q[1];
+}
+
+// One ray query.  ANY = true: trace_shadow_ray (path_tracer.hh:415-427),
+// i.e. the first accepted candidate ends the walk.  ANY = false: closest hit
+// (proceed/confirm loop of trace_ray, path_tracer.hh:342-349).
+template<bool ANY, bool COUNT>
+PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, f3 o, f3 d, float tmin, float tmax,
+                 Hit& best, Counters& cnt)
+{
+    if(COUNT) cnt.queries++;
+    const f3 inv_w = V3(rcp_or_big(d.x), rcp_or_big(d.y), rcp_or_big(d.z));
+    const uint32_t tlas_base = tlas_offset * 8 + octant(d) * tlas_count - sc.tlas_link_base;
+
+    // active level state
+    const TravRec* recs = sc.tlas_trav + tlas_base;
+    f3 org = o, inv = inv_w;
+    uint32_t node = 0, count = tlas_count;
+    bool in_blas = false;
+    uint32_t tlas_resume = 0;     // TLAS node to continue with after the BLAS
+    // BLAS level extras
+    f3 S = V3(0, 0, 0);
+    int axis = 2;
+    uint32_t tri_base = 0, inst = 0xFFFFFFFFu;
+
+    best.thit = -1.0f;
+    best.bx = best.by = best.bz = 0.0f;
+    best.instance_id = 0xFFFFFFFFu;
+    best.primitive_id = 0;
+    best.back_face = false;
+
+    for(;;)
+    {
+        if(node >= count)
+        {
+            if(!in_blas) break;
+            // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
+            in_blas = false;
+            recs = sc.tlas_trav + tlas_base;
+            org = o;
+            inv = inv_w;
+            node = tlas_resume;
+            count = tlas_count;
+            continue;
+        }
+        float4 lo, hi;
+        load_trav(recs + node, lo, hi);
+        if(COUNT) cnt.visits++;
+        // slab test (ray_query.hh:197-207); min/max results only feed compares
+        const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
+        const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;
+        const float t0z = (lo.z - org.z) * inv.z, t1z = (hi.z - org.z) * inv.z;
+        const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
+        const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
+        const uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
+        if(!(nearv <= farv && farv > tmin && nearv < tmax)) { node = cancel; continue; }
+        if(!(accept & 0x80000000u)) { node = accept; continue; }
+        node = cancel;
+        const uint32_t leaf = accept & 0x7FFFFFFFu;
+        if(!in_blas)
+        {
+            // ray_query_enter_blas (ray_query.hh:153-182)
+            if(COUNT) cnt.blas_entries++;
+            const float4* ip = reinterpret_cast<const float4*>(sc.inst_trav + leaf);
+            const float4 a = ip[0], b = ip[1], c = ip[2], e = ip[3];
+            // a = M0.xyz M1.x | b = M1.yz M2.xy | c = M2.z M3.xyz | e = blas count, offset, tri_base
+            const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(a.w, b.x, b.y), M2 = V3(b.z, b.w, c.x), M3 = V3(c.y, c.z, c.w);
+            const f3 bo = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
+                             M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
+                             M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
+            const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
+                             M0.y * d.x + M1.y * d.y + M2.y * d.z,
+                             M0.z * d.x + M1.z * d.y + M2.z * d.z);
+            const uint32_t bcount = __float_as_uint(e.x), boffset = __float_as_uint(e.y);
+            tri_base = __float_as_uint(e.z);
+            inst = leaf;
+            tlas_resume = node;
+            in_blas = true;
+            org = bo;
+            inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+            recs = sc.blas_trav + (boffset * 8 + octant(bd) * bcount);
+            count = bcount;
+            node = 0;
+            // ray_triangle_intersection_preprocess (math.hh:340-356)
+            const float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
+            f3 rd = bd;
+            axis = 2;
+            if(ax > ay && ax > az) { axis = 0; rd = V3(bd.z, bd.y, bd.x); }
+            else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
+            const float k = 1.0f / rd.z;
+            S = V3(rd.x * k, rd.y * k, 1.0f * k);
+            continue;
+        }
+        // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246, math.hh:358-401)
+        if(COUNT) cnt.tri_tests++;
+        const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + leaf);
+        const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+        const f3 A = V3(q0.x, q0.y, q0.z) - org, B = V3(q0.w, q1.x, q1.y) - org, C = V3(q1.z, q1.w, q2.x) - org;
+        f3 x = V3(A.x, B.x, C.x), y = V3(A.y, B.y, C.y), z = V3(A.z, B.z, C.z);
+        if(axis == 0) { x = z; z = V3(A.x, B.x, C.x); }
+        else if(axis == 1) { y = z; z = V3(A.y, B.y, C.y); }
+        x = x - S.x * z;
+        y = y - S.y * z;
+        const f3 uvw = cross(y, x);
+        const float det = uvw.x + uvw.y + uvw.z;
+        const float rdet = 1.0f / det;
+        const float u = uvw.x * rdet, v = uvw.y * rdet, t = dot(uvw, S.z * z) * rdet;
+        bool back = det < 0;
+        if(S.z < 0) back = !back;
+        if(axis != 2) back = !back;
+        const bool hit = det != 0.0f && t >= 0.0f &&
+                         ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
+                          (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f));
+        if(hit && t < tmax && t > tmin)
+        {
+            if(ANY) return true;
+            // ray_query_confirm (ray_query.hh:280-290)
+            best.bx = u;
+            best.by = v;
+            best.bz = 1.0f - u - v;
+            best.thit = t;
+            best.instance_id = inst;
+            best.primitive_id = leaf;
+            best.back_face = back;
+            tmax = t;
+        }
+    }
+    return ANY ? false : best.thit >= 0.0f;
+}
+
+struct HitInfo {
+    float thit;
+    f3 pos;
+    m3 tbn;
+    f3 albedo;
+    float roughness, metallic, emission, transmission, eta, nee_pdf;
+};
+
+struct Light {
+    f3 dir, color;
+    float cos;
+};
+
+PTG_D f3 ld3(const float* base, uint32_t i)
+{
+    const float4 v = reinterpret_cast<const float4*>(base)[i];
+    return V3(v.x, v.y, v.z);
+}
+PTG_D float4 ld4(const float* base, uint32_t i) { return reinterpret_cast<const float4*>(base)[i]; }
+
+// trace_ray (path_tracer.hh:340-412)
+template<bool COUNT>
+PTG_D HitInfo trace_ray(const DevScene& sc, uint32_t tc, uint32_t to, const Light& L, f3 origin, f3 dir, float tmin,
+                        Counters& cnt)
+{
+    Hit h;
+    trace<false, COUNT>(sc, tc, to, origin, dir, tmin, 1e9f, h, cnt);
+    HitInfo hi;
+    hi.thit = h.thit;
+    hi.nee_pdf = 0;
+    if(hi.thit < 0)
+    {
+        const float visible = dot(L.dir, dir) > L.cos ? 1.0f : 0.0f;
+        hi.nee_pdf = visible / (2.0f * PI_F * (1.0f - L.cos));
+        const float w = hi.nee_pdf == 0.0f ? 1.0f : hi.nee_pdf;
+        hi.albedo = V3(0.0f, 0.0f, 0.0f) + (visible * L.color) * w;
+        hi.emission = 1.0f;
+        hi.pos = V3(0, 0, 0);
+        hi.tbn = m3{{V3(0, 0, 0), V3(0, 0, 0), V3(0, 0, 0)}};
+        hi.roughness = hi.metallic = hi.transmission = hi.eta = 0.0f;
+        return hi;
+    }
+    if(COUNT) cnt.shades++;
+    hi.pos = origin + dir * h.thit;
+    const float4* sp = reinterpret_cast<const float4*>(sc.inst_shade + h.instance_id);
+    const float4 s0 = sp[0], s1 = sp[1], s2 = sp[2];
+    const m3 rot{{V3(s0.x, s0.y, s0.z), V3(s0.w, s1.x, s1.y), V3(s1.z, s1.w, s2.x)}};
+    const uint32_t ioff = __float_as_uint(s2.y), bv = __float_as_uint(s2.z);
+    const uint32_t tri = ioff + h.primitive_id * 3;
+    const uint32_t i0 = sc.indices[tri] + bv, i1 = sc.indices[tri + 1] + bv, i2 = sc.indices[tri + 2] + bv;
+    const f3 n0 = ld3(sc.normal, i0), n1 = ld3(sc.normal, i1), n2 = ld3(sc.normal, i2);
+    const float4 a0 = ld4(sc.albedo, i0), a1 = ld4(sc.albedo, i1), a2 = ld4(sc.albedo, i2);
+    const float4 m0 = ld4(sc.material, i0), m1 = ld4(sc.material, i1), m2 = ld4(sc.material, i2);
+    const float bx = h.bx, by = h.by, bz = h.bz;
+    hi.albedo = V3(a0.x * bx + a1.x * by + a2.x * bz, a0.y * bx + a1.y * by + a2.y * bz, a0.z * bx + a1.z * by + a2.z * bz);
+    const float mx = m0.x * bx + m1.x * by + m2.x * bz;
+    hi.metallic = m0.y * bx + m1.y * by + m2.y * bz;
+    hi.transmission = m0.z * bx + m1.z * by + m2.z * bz;
+    hi.emission = m0.w * bx + m1.w * by + m2.w * bz;
+    f3 n = (n0 * bx + n1 * by) + n2 * bz;
+    n = normalize(mul_m3v3(rot, n));
+    const float ior = 1.5f;
+    if(h.back_face) { hi.eta = ior; n = -n; }
+    else hi.eta = 1.0f / ior;
+    hi.tbn = tangent_space(n);
+    hi.roughness = mx * mx;
+    return hi;
+}
+
+// ---- samplers (path_tracer.hh:12-83) ----
+PTG_D float inv_erf(float x)                                          // math.hh:455-463
+{
+    const float ln1x2 = (float)dlog((double)(1 - x * x));
+    const float a = 0.147f;
+    const float p = 2.0f / (PI_F * a);
+    const float k = p + ln1x2 * 0.5f;
+    const float k2 = k * k;
+    const double inner = dsqrt((double)(k2 - ln1x2 * (1.0f / a)));
+    return (float)((double)signf(x) * dsqrt(inner - (double)k));
+}
+PTG_D f2 gaussian_disk(f2 u, float sigma)                              // :19-25 with sample_gaussian :12-17
+{
+    float r = fsqrt(u.x);
+    const float theta = 2.0f * PI_F * u.y;
+    float kk = r * 2.0f - 1.0f;
+    kk = clampf(kk, -(1.0f - 1e-6f), 1.0f - 1e-6f);
+    r = sigma * 1.41421356f * inv_erf(kk);
+    return f2{r * fcos(theta), r * fsin(theta)};
+}
+PTG_D f3 cosine_hemisphere(f2 u)                                       // :27-33
+{
+    const float r = fsqrt(u.x);
+    const float theta = 2.0f * PI_F * u.y;
+    const f2 d{r * fcos(theta), r * fsin(theta)};
+    return V3(d.x, d.y, fsqrt(gmax(0.0f, 1.0f - (d.x * d.x + d.y * d.y))));
+}
+PTG_D float cosine_pdf(f3 d) { return gmax(d.z * (1.0f / PI_F), 0.0f); }   // :35-38
+PTG_D f3 sample_cone(f3 dir, float cos_min, f2 u)                      // :40-48
+{
+    const float ct = mixf(1.0f, cos_min, u.x);
+    const float st = fsqrt(1.0f - ct * ct);
+    const float phi = u.y * 2.0f * PI_F;
+    return mul_m3v3(tangent_space(dir), V3(fcos(phi) * st, fsin(phi) * st, ct));
+}
+PTG_D f2 regular_polygon(f2 u, float angle, uint32_t sides)            // :50-62
+{
+    const float side = (float)floor((double)(u.x * (float)sides));
+    u.x *= (float)sides;
+    u.x = (float)((double)u.x - floor((double)u.x));
+    const float side_radians = (2.0f * PI_F) / (float)sides;
+    const float a1 = side_radians * side + angle;
+    const float a2 = side_radians * (side + 1.0f) + angle;
+    const f2 b{fsin(a1), fcos(a1)}, c{fsin(a2), fcos(a2)};
+    if(u.x + u.y > 1.0f) { u.x = 1.0f - u.x; u.y = 1.0f - u.y; }
+    return f2{b.x * u.x + c.x * u.y, b.y * u.x + c.y * u.y};
+}
+PTG_D f3 ggx_vndf(f3 view, float roughness, f2 u)                       // :67-83
+{
+    if(roughness < 1e-3f) return V3(0, 0, 1);
+    const f3 v = normalize(V3(roughness * view.x, roughness * view.y, view.z));
+    const float phi = 2.0f * PI_F * u.x;
+    const float z = (float)fma((double)(1.0f - u.y), (double)(1.0f + v.z), (double)(-v.z));
+    const float sin_theta = fsqrt(clampf(1.0f - z * z, 0.0f, 1.0f));
+    const float x = (float)((double)sin_theta * dcos((double)phi));
+    const float y = (float)((double)sin_theta * dsin((double)phi));
+    const f3 h = V3(x, y, z) + v;
+    return normalize(V3(roughness * h.x, roughness * h.y, gmax(0.0f, h.z)));
+}
+
+// ---- materials (path_tracer.hh:89-296) ----
+PTG_D float fresnel_att(float vdh, float f0, float eta, float roughness)     // :89-98
+{
+    if(eta > 1.0f)
+    {
+        const float s2 = eta * eta * (1.0f - vdh * vdh);
+        if(s2 >= 1.0f) return 1.0f;
+        vdh = fsqrt(1.0f - s2);
+    }
+    return (float)((double)f0 + (double)(gmax(1.0f - roughness, f0) - f0) * dpow((double)gmax(1.0f - vdh, 0.0f), 5.0));
+}
+PTG_D float tr_distribution(float hdotn, float a)                            // :105-110
+{
+    const float a2 = a * a;
+    const float denom = hdotn * hdotn * (a2 - 1.0f) + 1.0f;
+    return a2 / gmax(PI_F * denom * denom, 1e-10f);
+}
+PTG_D float tr_masking_shadowing(float ldotn, float ldoth, float vdotn, float vdoth, float a)   // :112-123
+{
+    if(vdotn * vdoth < 0) return 0;
+    if(ldotn * ldoth < 0) return 0;
+    const double l = fabs((double)vdotn) * dsqrt((double)(ldotn * ldotn - a * a * ldotn * ldotn + a * a));
+    const double v = fabs((double)ldotn) * dsqrt((double)(vdotn * vdotn - a * a * vdotn * vdotn + a * a));
+    return (float)(0.5 / (l + v));
+}
+PTG_D float tr_masking(float vdotn, float vdoth, float a)                    // :125-129
+{
+    if(vdotn * vdoth < 0) return 0;
+    return (float)((double)(2.0f * vdotn) / ((double)vdotn + dsqrt((double)(vdotn * vdotn * (1.0f - a * a) + a * a))));
+}
+
+struct Material {
+    f3 albedo;
+    float roughness, metallic, transmission, eta;
+};
+
+// bsdf_core (:131-181)
+PTG_D f3 bsdf_core(f3 light, f3 h, f3 view, const Material& M, float f0, float distribution, float& rpdf,
+                   float& dpdf, float& tpdf)
+{
+    const float ldotn = light.z, vdotn = view.z;
+    const float vdoth = dot(view, h), ldoth = dot(light, h);
+    const float fresnel = fresnel_att(vdoth, f0, M.eta, 0);
+    const float geometry = tr_masking_shadowing(ldotn, ldoth, vdotn, vdoth, M.roughness);
+    const float G1 = tr_masking(vdotn, vdoth, M.roughness);
+    f3 color;
+    if(light.z > 0)
+    {
+        const float spec = fresnel * (1.0f - M.metallic);
+        color = V3((M.albedo.x * M.metallic + spec) * geometry * distribution,
+                   (M.albedo.y * M.metallic + spec) * geometry * distribution,
+                   (M.albedo.z * M.metallic + spec) * geometry * distribution);
+        const float diffuse = (1.0f - fresnel) * (1.0f - M.metallic) * (1.0f - M.transmission) / PI_F;
+        color = color + diffuse * M.albedo;
+        rpdf = G1 * distribution / (4.0f * view.z);
+        dpdf = cosine_pdf(light);
+        tpdf = 0;
+    }
+    else
+    {
+        const float denom = M.eta * vdoth + ldoth;
+        const double k = (double)M.transmission * fabs((double)(vdoth * ldoth)) * (double)(1.0f - fresnel) * 4.0 *
+                         (double)geometry * (double)distribution / (double)(denom * denom);
+        color = M.albedo * (float)k;
+        rpdf = 0;
+        dpdf = 0;
+        tpdf = (float)(fabs((double)(vdoth * ldoth)) * (double)G1 * (double)distribution /
+                       (fabs((double)view.z) * (double)denom * (double)denom));
+    }
+    return color * fabsf(ldotn);
+}
+
+PTG_D void lobe_probs(f3 view, const Material& M, float& f0, float& rp, float& tp, float& dp)
+{
+    float f = (1.0f - M.eta) / (1.0f + M.eta);
+    f *= f;
+    f0 = f;
+    const float lum = dot(M.albedo, V3(0.2126f, 0.7152f, 0.0722f));
+    rp = mixf(1.0f, fresnel_att(view.z, f, M.eta, M.roughness), lum * (1.0f - M.metallic));
+    tp = (float)((1.0 - (double)rp) * (double)M.transmission);
+    dp = (float)((1.0 - (double)rp) * (double)(1.0f - M.transmission));
+}
+
+// bsdf (:184-222)
+PTG_D f3 bsdf_eval(f3 light, f3 view, const Material& M, float& out_pdf)
+{
+    f3 h;
+    if(light.z > 0) h = normalize(view + light);
+    else h = signf(M.eta - 1.0f) * normalize(light + M.eta * view);
+    const float distribution = tr_distribution(h.z, M.roughness);
+    float f0, rp, tp, dp;
+    lobe_probs(view, M, f0, rp, tp, dp);
+    float r, d, t;
+    const f3 att = bsdf_core(light, h, view, M, f0, M.roughness < 1e-3f ? 0.0f : distribution, r, d, t);
+    out_pdf = r * rp + d * dp + t * tp;
+    return att;
+}
+
+// sample_bsdf (:224-296)
+PTG_D void bsdf_sample(f3 u, f3 view, const Material& M, f3& out_dir, f3& out_att, float& out_pdf)
+{
+    const f2 uxy{u.x, u.y};
+    f3 h = ggx_vndf(view, M.roughness, uxy);
+    float f0, rp, tp, dp;
+    lobe_probs(view, M, f0, rp, tp, dp);
+    bool diffuse = false, bad;
+    if((u.z -= rp) <= 0)
+    {   // reflect(-view, h) (math.hh:442-445)
+        const f3 I = -view;
+        out_dir = I - (2.0f * dot(h, I)) * h;
+        bad = out_dir.z <= 0;
+    }
+    else if((u.z -= tp) <= 0)
+    {   // refract(-view, h, eta) (math.hh:447-453)
+        const f3 I = -view;
+        const float ndoti = dot(h, I);
+        const float k = 1.0f - M.eta * M.eta * (1.0f - ndoti * ndoti);
+        if(k < 0.0f) out_dir = V3(0, 0, 0);
+        else
+        {
+            const float s = (float)((double)(M.eta * ndoti) + dsqrt((double)k));
+            out_dir = M.eta * I - s * h;
+        }
+        bad = out_dir.z >= 0;
+    }
+    else
+    {
+        out_dir = cosine_hemisphere(uxy);
+        h = normalize(out_dir + view);
+        diffuse = true;
+        bad = out_dir.z == 0;
+    }
+    if(bad)
+    {
+        out_dir = V3(0, 0, 1);
+        out_att = V3(0, 0, 0);
+        out_pdf = 1;
+        return;
+    }
+    float distribution = tr_distribution(h.z, M.roughness);
+    if(M.roughness < 1e-3f) distribution = diffuse ? 0 : fabsf(4.0f * out_dir.z * view.z);
+    float r, d, t;
+    out_att = bsdf_core(out_dir, h, view, M, f0, distribution, r, d, t);
+    out_pdf = r * rp + t * tp;
+    if(M.roughness < 1e-3f && !diffuse) out_pdf = -out_pdf;
+    else out_pdf += d * dp;
+}
+
+// ray_sphere_intersection (math.hh:404-417)
+PTG_D bool ray_sphere(f3 o, f3 d, f3 c, float radius, float& tmin, float& tmax)
+{
+    const f3 oc = o - c;
+    const float b = dot(oc, d);
+    const float cc = dot(oc, oc) - radius * radius;
+    float disc = b * b - cc;
+    if(disc < 0) return false;
+    disc = fsqrt(disc);
+    tmin = -b - disc;
+    tmax = -b + disc;
+    return true;
+}
+
+constexpr float RAY_R = 5.8e-6f, RAY_G = 13.6e-6f, RAY_B = 33.1e-6f, MIE_K = 4.0e-6f;
+
+// nishita_atmosphere_attenuation (:456-497)
+PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
+{
+    const f3 earth = V3(0, -EARTH_RADIUS, 0);
+    float tmin = 0, atmax = 0;
+    if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return V3(1.0f, 1.0f, 1.0f);
+    tmin = (float)gmax_d((double)tmin, 0.0);
+    tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
+    const float segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
+    float ray_depth = 0, mie_depth = 0;
+    bool shadowed = false;
+    for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
+    {
+        const float t = segment * (jitter + (float)i);
+        const float height = length((pos + t * view) - earth) - EARTH_RADIUS;
+        ray_depth = (float)((double)ray_depth + dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)));
+        mie_depth = (float)((double)mie_depth + dexp((double)(-height / MIE_SCALE_HEIGHT)));
+        if(height < 0) shadowed = true;
+    }
+    if(shadowed) return V3(0.0f, 0.0f, 0.0f);
+    const f3 tau = V3((RAY_R * ray_depth + MIE_K * mie_depth) * segment, (RAY_G * ray_depth + MIE_K * mie_depth) * segment,
+                      (RAY_B * ray_depth + MIE_K * mie_depth) * segment);
+    return V3(fexp(-tau.x), fexp(-tau.y), fexp(-tau.z));
+}
+
+// nishita_atmosphere_scattering (:499-588)
+PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, float tmax, f3& attenuation, f3& in_scatter)
+{
+    const f3 earth = V3(0, -EARTH_RADIUS, 0);
+    attenuation = V3(1.0f, 1.0f, 1.0f);
+    in_scatter = V3(0.0f, 0.0f, 0.0f);
+    if(tmax > 0 && tmax < 1e3f) return;
+    float tmin = 0, atmax = 0;
+    if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return;
+    tmin = (float)gmax_d((double)tmin, 0.0);
+    tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
+    const float segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
+    const f4 jitter = uniform4(seed);
+    const float mu = dot(view, L.dir);
+    const float rayleigh_phase = 3.0f / (16.0f * PI_F) * (1.0f + mu * mu);
+    const float g = MIE_ANISOTROPY;
+    const float mie_phase = (float)((double)(3.0f / (8.0f * PI_F) * (1.0f - g * g) * (1.0f + mu * mu)) /
+                                    ((double)(2.0f + g * g) * dpow((double)(1.0f + g * g - 2.0f * g * mu), 1.5)));
+    float ray_depth = 0, mie_depth = 0;
+    f3 ray_sum = V3(0, 0, 0), mie_sum = V3(0, 0, 0);
+    for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
+    {
+        const float t = segment * (jitter.x + (float)i);
+        const f3 p = pos + t * view;
+        ray_sphere(p, L.dir, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, tmax);   // keeps old values on a miss
+        const float light_segment = (tmax - tmin) / (float)SECONDARY_ITERATIONS;
+        float lray = 0, lmie = 0;
+        bool shadowed = false;
+        for(int j = 0; j < SECONDARY_ITERATIONS; ++j)
+        {
+            const float tt = light_segment * (jitter.y + (float)j);
+            const float height = length((p + tt * L.dir) - earth) - EARTH_RADIUS;
+            lray = (float)((double)lray + dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)));
+            lmie = (float)((double)lmie + dexp((double)(-height / MIE_SCALE_HEIGHT)));
+            if(height < 0) shadowed = true;
+        }
+        const float height = gmax(length(p - earth) - EARTH_RADIUS, 0.0f);
+        const float ray_density = (float)(dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)) * (double)segment);
+        const float mie_density = (float)(dexp((double)(-height / MIE_SCALE_HEIGHT)) * (double)segment);
+        ray_depth += ray_density;
+        mie_depth += mie_density;
+        const float kr = lray * light_segment + ray_depth, km = lmie * light_segment + mie_depth;
+        f3 local = V3(0.0f, 0.0f, 0.0f);
+        if(!shadowed)
+            local = V3(fexp(-(RAY_R * kr + MIE_K * km)), fexp(-(RAY_G * kr + MIE_K * km)), fexp(-(RAY_B * kr + MIE_K * km)));
+        ray_sum = ray_sum + local * ray_density;
+        mie_sum = mie_sum + local * mie_density;
+    }
+    attenuation = V3(fexp(-(RAY_R * ray_depth + MIE_K * mie_depth)), fexp(-(RAY_G * ray_depth + MIE_K * mie_depth)),
+                     fexp(-(RAY_B * ray_depth + MIE_K * mie_depth)));
+    const f3 R = V3(RAY_R, RAY_G, RAY_B), Mk = V3(MIE_K, MIE_K, MIE_K);
+    in_scatter = ((((ray_sum * R) * rayleigh_phase) + ((mie_sum * Mk) * mie_phase)) * L.color) * 4.0f;
+}
+
+// nee_branch (:594-620)
+template<bool COUNT>
+PTG_D f3 nee_branch(const DevScene& sc, uint32_t tc, uint32_t to, u4& seed, const Light& L, const HitInfo& info,
+                    const Material& M, f3 tview, Counters& cnt)
+{
+    const f4 u = uniform4(seed);
+    const f3 light_dir = sample_cone(L.dir, L.cos, f2{u.x, u.y});
+    const float nee_pdf = 1.0f / (2.0f * PI_F * (1.0f - L.cos));
+    float bsdf_pdf = 0;
+    const f3 b = bsdf_eval(mul_v3m3(light_dir, info.tbn), tview, M, bsdf_pdf);
+    f3 color = (b * nee_pdf) * L.color;
+    if(color.x == 0 && color.y == 0 && color.z == 0) return V3(0, 0, 0);
+    Hit unused;
+    if(trace<true, COUNT>(sc, tc, to, info.pos, light_dir, MIN_RAY_DIST, MAX_RAY_DIST, unused, cnt)) return V3(0, 0, 0);
+    float mis_pdf = 1.0f;
+    if(L.cos < 1.0f) mis_pdf = (nee_pdf * nee_pdf + bsdf_pdf * bsdf_pdf) / nee_pdf;
+    color = color * atmosphere_attenuation(u.w, info.pos, light_dir, MAX_RAY_DIST);
+    return color / mis_pdf;
+}
+
+PTG_D float rd_f(const uint8_t* p, uint32_t off) { return *reinterpret_cast<const float*>(p + off); }
+PTG_D uint32_t rd_u(const uint8_t* p, uint32_t off) { return *reinterpret_cast<const uint32_t*>(p + off); }
+PTG_D f3 rd_f3(const uint8_t* p, uint32_t off)
+{
+    const float4 v = *reinterpret_cast<const float4*>(p + off);
+    return V3(v.x, v.y, v.z);
+}
+
+// path_trace_pixel (path_tracer.hh:637-741)
+template<bool COUNT>
+PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
+{
+    const uint32_t sub = sample_index < 0 ? 0u : (uint32_t)sample_index / sc.blur_step;
+    const uint8_t* sf = sc.subframes + size_t(sub) * SF_STRIDE;
+    const uint32_t tc = rd_u(sf, SF_TLAS), to = rd_u(sf, SF_TLAS + 4);
+    Light L;
+    L.dir = rd_f3(sf, SF_LIGHT);
+    L.color = rd_f3(sf, SF_LIGHT + 16);
+    L.cos = rd_f(sf, SF_LIGHT + 32);
+
+    u4 seed{px, py, (uint32_t)sample_index, sc.student_id};
+    pcg4d(seed);
+    const f4 u = uniform4(seed);
+    f2 film = gaussian_disk(f2{u.x, u.y}, 0.4f);
+    film.x = film.x + 0.5f;
+    film.y = film.y + 0.5f;
+
+    // get_camera_ray (:429-450)
+    const uint8_t* cam = sf + SF_CAM;
+    f3 ray_dir, ray_o;
+    {
+        float uvx = ((float)px + film.x) / (float)sc.width * 2.0f - 1.0f;
+        float uvy = ((float)py + film.y) / (float)sc.height * 2.0f - 1.0f;
+        uvx *= rd_f(cam, 64);
+        uvy = -uvy;
+        f2 ap{0, 0};
+        const int32_t polygon = (int32_t)rd_u(cam, 80);
+        if(polygon > 3)
+        {
+            const f2 p = regular_polygon(f2{u.z, u.w}, rd_f(cam, 76), (uint32_t)polygon);
+            const float rad = rd_f(cam, 84);
+            ap = f2{p.x * rad, p.y * rad};
+        }
+        const f3 origin = V3(ap.x, ap.y, 0.0f);
+        const float ifl = rd_f(cam, 68), fd = rd_f(cam, 72);
+        f3 d = V3(uvx * ifl * fd, uvy * ifl * fd, -1.0f * fd);
+        d = normalize(d - origin);
+        const m3 ori{{rd_f3(cam, 0), rd_f3(cam, 16), rd_f3(cam, 32)}};
+        ray_dir = mul_m3v3(ori, d);
+        ray_o = mul_m3v3(ori, origin) + rd_f3(cam, 48);
+    }
+
+    HitInfo info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, 0.0f, cnt);
+    f3 attenuation, in_scatter;
+    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, attenuation, in_scatter);
+    f3 contribution = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
+
+    float regularization = 1.0f;
+    for(uint32_t bounce = 0; bounce < sc.max_bounces && info.thit > 0; ++bounce)
+    {
+        Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
+        f3 view = mul_v3m3(-ray_dir, info.tbn);
+        if(view.z < 1e-7f) view.z = gmax(view.z, 1e-7f);
+        view = normalize(view);
+
+        contribution = contribution + attenuation * nee_branch<COUNT>(sc, tc, to, seed, L, info, M, view, cnt);
+
+        const f4 ub = uniform4(seed);
+        f3 tdir, batt;
+        float bpdf;
+        bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf);
+        ray_dir = normalize(mul_m3v3(info.tbn, tdir));
+        ray_o = info.pos;
+        info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, MIN_RAY_DIST, cnt);
+
+        const float mis_pdf = bpdf < 0 ? -bpdf : (info.nee_pdf * info.nee_pdf + bpdf * bpdf) / bpdf;
+        attenuation = attenuation * batt;
+        f3 aatt, insc;
+        atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc);
+        const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
+        contribution = contribution + term / mis_pdf;
+        attenuation = attenuation * (aatt / fabsf(bpdf));
+        if(bpdf > 0.0f)
+            regularization = (float)((double)regularization *
+                                     gmax_d(1.0 - (double)REGULARIZATION_GAMMA / dpow((double)bpdf, 0.25), 0.0));
+        info.roughness = 1.0f - (1.0f - info.roughness) * regularization;
+    }
+    return contribution;
+}
+
+// tonemap_pixel (:753-771): ACES fit, sRGB curve, clamp, BGRA
+PTG_D float aces(float c) { return (c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f); }
+PTG_D float srgb(float c)
+{
+    return c < 0.0031308f ? c * 12.92f
+                          : (float)(dpow((double)c, (double)(1.0f / 2.4f)) * (double)1.055f - (double)0.055f);
+}
+PTG_D uchar4 tonemap(f3 c)
+{
+    const float r = clampf(srgb(aces(c.x)), 0.0f, 1.0f);
+    const float g = clampf(srgb(aces(c.y)), 0.0f, 1.0f);
+    const float b = clampf(srgb(aces(c.z)), 0.0f, 1.0f);
+    return make_uchar4((unsigned char)roundf(b * 255.0f), (unsigned char)roundf(g * 255.0f),
+                       (unsigned char)roundf(r * 255.0f), 255);
+}
+
+} // namespace dm
+} // namespace ptg

@@ -1,0 +1,111 @@
+// Device arithmetic with the reference's exact semantics (gfx950).
+//
+// The hot path must reproduce the reference's float results bit for bit, so
+// this header pins down every operation whose result could otherwise differ
+// from the reference's C++ on the CPU:
+//   * kernels are compiled with -ffp-contract=off (no silent FMA) and
+//     without fast-math; f32 division and sqrt are correctly rounded (HIP's
+//     default -fhip-fp32-correctly-rounded-divide-sqrt), denormals kept;
+//   * the reference's unqualified exp/log/pow/sin/cos/fma on a float run in
+//     DOUBLE (math.hh imports only fmin/fmax as float overloads), so do ours:
+//     ocml's f64 routines, result rounded to float exactly where the
+//     reference assigns to a float;
+//   * fminf/fmaxf keep glibc's tie rule (equal operands -> the second one),
+//     which decides the sign of a zero; NaN operands are dropped as in C.
+// Only the slab test (whose min/max feed comparisons alone) uses the raw
+// v_min/v_max instructions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptg {
+namespace dm {
+
+#define PTG_D __device__ __forceinline__
+
+struct f2 { float x, y; };
+struct f3 { float x, y, z; };
+struct f4 { float x, y, z, w; };
+struct m3 { f3 r[3]; };
+struct u4 { uint32_t x, y, z, w; };
+
+constexpr double PI_D = 3.14159265358979323846;
+constexpr float PI_F = (float)PI_D;
+
+PTG_D f3 V3(float x, float y, float z) { return f3{x, y, z}; }
+PTG_D f3 operator+(f3 a, f3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PTG_D f3 operator-(f3 a, f3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PTG_D f3 operator*(f3 a, f3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+PTG_D f3 operator*(f3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+PTG_D f3 operator*(float s, f3 a) { return V3(s * a.x, s * a.y, s * a.z); }
+PTG_D f3 operator/(f3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+PTG_D f3 operator-(f3 a) { return V3(-a.x, -a.y, -a.z); }
+PTG_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PTG_D f3 cross(f3 a, f3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+
+// f32 sqrt: correctly rounded == the reference's (float)sqrt((double)x)
+PTG_D float fsqrt(float x) { return __builtin_sqrtf(x); }
+PTG_D float length(f3 a) { return fsqrt(dot(a, a)); }
+PTG_D f3 normalize(f3 a) { return a / length(a); }
+
+// glibc fminf/fmaxf (x86_64 minss/maxss + NaN fix-up): ties return y.
+PTG_D float gmin(float x, float y) { return (x < y || y != y) ? x : y; }
+PTG_D float gmax(float x, float y) { return (x > y || y != y) ? x : y; }
+PTG_D double gmax_d(double x, double y) { return (x > y || y != y) ? x : y; }
+PTG_D float clampf(float v, float lo, float hi) { return gmin(gmax(v, lo), hi); }
+PTG_D float mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+PTG_D float signf(float v)
+{
+    if(v < 0) return -1.0f;
+    if(v > 0) return 1.0f;
+    return v == -0.0f ? -0.0f : +0.0f;
+}
+
+// double-precision library calls, as the reference makes them
+PTG_D double dexp(double x) { return exp(x); }
+PTG_D double dlog(double x) { return log(x); }
+PTG_D double dpow(double x, double y) { return pow(x, y); }
+PTG_D double dsin(double x) { return sin(x); }
+PTG_D double dcos(double x) { return cos(x); }
+PTG_D double dsqrt(double x) { return sqrt(x); }
+PTG_D float fcos(float x) { return (float)dcos((double)x); }
+PTG_D float fsin(float x) { return (float)dsin((double)x); }
+PTG_D float fexp(float x) { return (float)dexp((double)x); }
+
+PTG_D f3 mul_v3m3(f3 b, const m3& a) { return V3(dot(a.r[0], b), dot(a.r[1], b), dot(a.r[2], b)); }
+PTG_D f3 mul_m3v3(const m3& b, f3 a)
+{
+    m3 t{{V3(b.r[0].x, b.r[1].x, b.r[2].x), V3(b.r[0].y, b.r[1].y, b.r[2].y), V3(b.r[0].z, b.r[1].z, b.r[2].z)}};
+    return mul_v3m3(a, t);
+}
+
+// create_tangent_space (math.hh:419-435); threshold compared in double
+PTG_D m3 tangent_space(f3 n)
+{
+    f3 major;
+    if(fabs((double)n.x) < 0.57735026918962576451) major = V3(1, 0, 0);
+    else if(fabs((double)n.y) < 0.57735026918962576451) major = V3(0, 1, 0);
+    else major = V3(0, 0, 1);
+    f3 t = normalize(cross(n, major));
+    f3 b = cross(n, t);
+    return m3{{t, b, n}};
+}
+
+// pcg4d (math.hh:466-473), simultaneous updates
+PTG_D void pcg4d(u4& s)
+{
+    uint32_t x = s.x * 1664525u + 1013904223u, y = s.y * 1664525u + 1013904223u;
+    uint32_t z = s.z * 1664525u + 1013904223u, w = s.w * 1664525u + 1013904223u;
+    uint32_t a = x + y * w, b = y + z * x, c = z + x * y, d = w + y * z;
+    a ^= a >> 16u; b ^= b >> 16u; c ^= c >> 16u; d ^= d >> 16u;
+    s.x = a + b * d; s.y = b + c * a; s.z = c + a * b; s.w = d + b * c;
+}
+PTG_D f4 uniform4(u4& s)
+{
+    pcg4d(s);
+    const float k = 2.3283064365386963e-10f;
+    return f4{(float)s.x * k, (float)s.y * k, (float)s.z * k, (float)s.w * k};
+}
+
+} // namespace dm
+} // namespace ptg

@@ -1,0 +1,814 @@
+// HIP kernels + C ABI of the GPU renderer (include/ptg.h).
+//
+//   k_pack_bvh      reference nodes + 8 link orders -> TravRec (32 B / visit)
+//   k_pack_tris     indices + positions -> TriRec (48 B / triangle)
+//   k_trace         path_trace_pixel for a (pixel set x sample chunk) grid,
+//                   one work-item per (pixel, sample); results to a
+//                   [sample][pixel] float4 buffer in HBM
+//   k_accumulate    baseline_render's j-ordered float32 sum over the chunk,
+//                   then (last chunk) / SPP + tonemap_pixel (main.cc:24-43)
+//   k_sample_list   path_trace_pixel for an explicit (x, y, j) list (parity)
+//   k_rays          ray_query closest hit + shadow any-hit (parity)
+//   k_tonemap, k_scatter_tiles
+//
+// No fallback path exists: every entry point fails loudly (negative code +
+// ptg_last_error) when HIP or the device is unavailable.
+#include <hip/hip_runtime.h>
+#include "ptg.h"
+#include "device/layout.h"
+#include "device/path_tracer.h"
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+namespace ptg {
+void set_last_error(const std::string& msg);   // scene.cpp
+}
+
+using namespace ptg;
+using namespace ptg::dm;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------- kernels --
+
+struct BvhJob {
+    uint32_t node_begin;   // first node in the raw node array
+    uint32_t link_begin;   // first link in the raw link array (8 orders follow)
+    uint32_t count;        // nodes in this BVH
+    uint32_t out_begin;    // first record in the output TravRec array
+};
+
+__global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh_link* __restrict__ links,
+                           TravRec* __restrict__ out, const BvhJob* __restrict__ jobs)
+{
+    const BvhJob j = jobs[blockIdx.y];
+    const uint32_t total = 8u * j.count;
+    for(uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x)
+    {
+        const uint32_t i = k % j.count;
+        const ptg_bvh_node n = nodes[j.node_begin + i];
+        const ptg_bvh_link l = links[j.link_begin + k];
+        TravRec r;
+        r.min_x = n.min_x; r.min_y = n.min_y; r.min_z = n.min_z; r.accept = l.accept;
+        r.max_x = n.max_x; r.max_y = n.max_y; r.max_z = n.max_z; r.cancel = l.cancel;
+        out[j.out_begin + k] = r;
+    }
+}
+
+struct MeshJob {
+    uint32_t index_offset, triangle_count, base_vertex_offset, pad;
+};
+
+__global__ void k_pack_tris(const uint32_t* __restrict__ indices, const float4* __restrict__ pos, TriRec* __restrict__ out,
+                            const MeshJob* __restrict__ jobs)
+{
+    const MeshJob j = jobs[blockIdx.y];
+    for(uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < j.triangle_count; t += gridDim.x * blockDim.x)
+    {
+        const uint32_t* tri = indices + j.index_offset + 3u * t;
+        const float4 a = pos[j.base_vertex_offset + tri[0]];
+        const float4 b = pos[j.base_vertex_offset + tri[1]];
+        const float4 c = pos[j.base_vertex_offset + tri[2]];
+        TriRec r;
+        r.p0x = a.x; r.p0y = a.y; r.p0z = a.z; r.p1x = b.x;
+        r.p1y = b.y; r.p1z = b.z; r.p2x = c.x; r.p2y = c.y;
+        r.p2z = c.z; r.pad0 = 0; r.pad1 = 0; r.pad2 = 0;
+        out[j.index_offset / 3u + t] = r;
+    }
+}
+
+// Which image pixels a launch covers: a rectangle, or an interleaved tile set.
+struct PixelMap {
+    uint32_t tiles;                 // 0: rectangle, 1: tiles
+    uint32_t x0, y0, w, h;          // rectangle
+    uint32_t tw, th, tiles_x, first, stride;
+    uint32_t img_w, img_h;
+    uint32_t npix;
+
+    __device__ __forceinline__ bool pixel(uint32_t p, uint32_t& x, uint32_t& y) const
+    {
+        if(!tiles)
+        {
+            x = x0 + p % w;
+            y = y0 + p / w;
+            return true;
+        }
+        const uint32_t per = tw * th;
+        const uint32_t t = first + (p / per) * stride;
+        const uint32_t q = p % per;
+        x = (t % tiles_x) * tw + q % tw;
+        y = (t / tiles_x) * th + q / tw;
+        return x < img_w && y < img_h;
+    }
+};
+
+struct CounterSink {
+    unsigned long long* dev;   // [8]
+};
+
+__device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* dev, uint32_t samples)
+{
+    atomicAdd(dev + 0, (unsigned long long)samples);
+    atomicAdd(dev + 1, (unsigned long long)c.visits);
+    atomicAdd(dev + 2, (unsigned long long)c.tri_tests);
+    atomicAdd(dev + 3, (unsigned long long)c.blas_entries);
+    atomicAdd(dev + 4, (unsigned long long)c.queries);
+    atomicAdd(dev + 5, (unsigned long long)c.shades);
+}
+
+// One work-item per (pixel, sample).  A wave holds 8 pixels x 8 consecutive
+// samples (one motion-blur subframe): lanes 0-7 are samples j..j+7 of pixel 0,
+// and so on.  Consecutive waves walk the sample groups of one pixel group, so
+// the waves in flight on a CU trace nearby pixels through the same TLASes.
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_trace(DevScene sc, PixelMap pm, uint32_t j0, uint32_t nj,
+                                                  float4* __restrict__ out, unsigned long long* __restrict__ counters)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t wave = g >> 6, lane = g & 63u;
+    const uint32_t sgroups = (nj + 7u) >> 3;
+    const uint32_t sg = wave % sgroups, pg = wave / sgroups;
+    const uint32_t jj = sg * 8u + (lane & 7u);
+    const uint32_t p = pg * 8u + (lane >> 3);
+    Counters cnt;
+    if(p < pm.npix && jj < nj)
+    {
+        uint32_t x, y;
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        if(pm.pixel(p, x, y))
+        {
+            const f3 c = path_trace_sample<COUNT>(sc, x, y, (int32_t)(j0 + jj), cnt);
+            r = make_float4(c.x, c.y, c.z, 0.f);
+        }
+        out[size_t(jj) * pm.npix + p] = r;
+        if(COUNT) flush_counters(cnt, counters, 1);
+    }
+}
+
+// acc[p] (+)= samples in index order; on the last chunk / spp and tonemap.
+__global__ __launch_bounds__(kBlock) void k_accumulate(PixelMap pm, uint32_t nj, const float4* __restrict__ samples,
+                                                       float4* __restrict__ acc, int first, int last, float spp,
+                                                       float4* __restrict__ out_accum, uchar4* __restrict__ out_bgra)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if(p >= pm.npix) return;
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    if(!first)
+    {
+        const float4 a = acc[p];
+        ax = a.x; ay = a.y; az = a.z;
+    }
+    for(uint32_t j = 0; j < nj; ++j)
+    {
+        const float4 s = samples[size_t(j) * pm.npix + p];
+        ax = ax + s.x;
+        ay = ay + s.y;
+        az = az + s.z;
+    }
+    if(!last)
+    {
+        acc[p] = make_float4(ax, ay, az, 0.f);
+        return;
+    }
+    ax = ax / spp;
+    ay = ay / spp;
+    az = az / spp;
+    uint32_t x, y;
+    const bool inside = pm.pixel(p, x, y);
+    if(out_accum) out_accum[p] = inside ? make_float4(ax, ay, az, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if(out_bgra) out_bgra[p] = inside ? tonemap(V3(ax, ay, az)) : make_uchar4(0, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_sample_list(DevScene sc, uint32_t n, const uint2* __restrict__ xy,
+                                                        const int32_t* __restrict__ js, float4* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if(i >= n) return;
+    Counters cnt;
+    const f3 c = path_trace_sample<false>(sc, xy[i].x, xy[i].y, js[i], cnt);
+    out[i] = make_float4(c.x, c.y, c.z, 0.f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_rays(DevScene sc, uint32_t tlas_count, uint32_t tlas_offset, uint32_t n,
+                                                 const float* __restrict__ rays, uint32_t* __restrict__ hits)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if(i >= n) return;
+    const float* r = rays + size_t(i) * 8;
+    const f3 o = V3(r[0], r[1], r[2]), d = V3(r[3], r[4], r[5]);
+    Counters cnt;
+    Hit h, unused;
+    trace<false, false>(sc, tlas_count, tlas_offset, o, d, r[6], r[7], h, cnt);
+    const bool shadow = trace<true, false>(sc, tlas_count, tlas_offset, o, d, r[6], r[7], unused, cnt);
+    uint32_t* w = hits + size_t(i) * 8;
+    w[0] = __float_as_uint(h.bx);
+    w[1] = __float_as_uint(h.by);
+    w[2] = __float_as_uint(h.bz);
+    w[3] = __float_as_uint(h.thit);
+    w[4] = h.instance_id;
+    w[5] = h.primitive_id;
+    w[6] = h.back_face ? 1u : 0u;
+    w[7] = shadow ? 1u : 0u;
+}
+
+__global__ void k_tonemap(uint32_t n, const float4* __restrict__ in, uchar4* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if(i < n) out[i] = tonemap(V3(in[i].x, in[i].y, in[i].z));
+}
+
+__global__ void k_scatter_tiles(PixelMap pm, const uchar4* __restrict__ tiles, uchar4* __restrict__ image)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if(p >= pm.npix) return;
+    uint32_t x, y;
+    if(pm.pixel(p, x, y)) image[size_t(y) * pm.img_w + x] = tiles[p];
+}
+
+// ---------------------------------------------------------------- runtime --
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if(p) (void)hipFree(p); }
+    hipError_t reserve(size_t n)
+    {
+        if(n <= bytes && p) return hipSuccess;
+        if(p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+        if(n == 0) return hipSuccess;
+        hipError_t e = hipMalloc(&p, n);
+        if(e == hipSuccess) bytes = n;
+        return e;
+    }
+    template<typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+int hip_fail(hipError_t e, const char* what)
+{
+    set_last_error(std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
+    return PTG_E_HIP;
+}
+
+#define PTG_HIP(call)                                                        \
+    do {                                                                     \
+        hipError_t e_ = (call);                                              \
+        if(e_ != hipSuccess) return hip_fail(e_, #call);                     \
+    } while(0)
+
+int fail(int code, const std::string& msg)
+{
+    set_last_error(msg);
+    return code;
+}
+
+uint32_t grid_for(size_t n, uint32_t block = kBlock) { return uint32_t((n + block - 1) / block); }
+
+} // namespace
+
+struct ptg_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool counting = false;
+    // static scene (reference layout) + repacked records
+    DevBuf nodes, links, indices, pos, normal, albedo, material;
+    DevBuf blas_trav, tris;
+    size_t static_nodes = 0, index_count = 0, vertex_count = 0;
+    std::unordered_set<uint32_t> packed_bvh, packed_mesh;
+    bool scene_ready = false;
+    // frame
+    DevBuf frame_nodes, frame_links, tlas_trav, subframes, inst_trav, inst_shade, jobs;
+    size_t first_frame_node = 0, frame_node_count = 0, subframe_count = 0, instance_count = 0;
+    std::vector<ptg_subframe> host_subframes;
+    bool frame_ready = false;
+    // render workspace
+    DevBuf samples, acc, tmp_a, tmp_b, tmp_c, counters;
+    uint64_t last_counters[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // k_trace launch timing (HIP events on the launch stream)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    size_t ev_used = 0;
+    ~ptg_context()
+    {
+        for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
+        for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
+    }
+
+    DevScene scene_args(const ptg_render_config* cfg) const
+    {
+        DevScene s;
+        s.blas_trav = blas_trav.as<TravRec>();
+        s.tlas_trav = tlas_trav.as<TravRec>();
+        s.tris = tris.as<TriRec>();
+        s.inst_trav = inst_trav.as<InstTrav>();
+        s.inst_shade = inst_shade.as<InstShade>();
+        s.indices = indices.as<uint32_t>();
+        s.normal = normal.as<float>();
+        s.albedo = albedo.as<float>();
+        s.material = material.as<float>();
+        s.subframes = subframes.as<uint8_t>();
+        s.tlas_link_base = uint32_t(8 * first_frame_node);
+        s.width = cfg ? cfg->width : 0;
+        s.height = cfg ? cfg->height : 0;
+        s.spp = cfg ? cfg->samples_per_pixel : 0;
+        s.max_bounces = cfg ? cfg->max_bounces : 0;
+        s.student_id = cfg ? cfg->student_id : 0;
+        s.blur_step = cfg ? cfg->samples_per_motion_blur_step : 8;
+        s.subframe_count = uint32_t(subframe_count);
+        return s;
+    }
+};
+
+namespace {
+
+int bind(ptg_context* ctx)
+{
+    if(!ctx) return fail(PTG_E_INVALID, "null context");
+    PTG_HIP(hipSetDevice(ctx->device));
+    return PTG_OK;
+}
+
+int check_cfg(const ptg_context* ctx, const ptg_render_config* cfg, uint32_t sample_end)
+{
+    if(!cfg || cfg->width == 0 || cfg->height == 0 || cfg->samples_per_pixel == 0 || cfg->samples_per_motion_blur_step == 0)
+        return fail(PTG_E_INVALID, "bad render config");
+    if(!ctx->scene_ready || !ctx->frame_ready) return fail(PTG_E_INVALID, "scene/frame not uploaded");
+    if(sample_end > 0)
+    {
+        const uint64_t need = (uint64_t(sample_end) - 1) / cfg->samples_per_motion_blur_step + 1;
+        if(need > ctx->subframe_count)
+            return fail(PTG_E_RANGE, "sample range needs " + std::to_string(need) + " subframes, frame has " +
+                                         std::to_string(ctx->subframe_count));
+    }
+    if(uint64_t(cfg->width) * cfg->height > (1ull << 31)) return fail(PTG_E_RANGE, "image too large");
+    return PTG_OK;
+}
+
+// Render the pixels of `pm` for samples [j0, j1): chunked trace + ordered accumulate.
+int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint32_t j0, uint32_t j1,
+               ptg_float4* out_accum, ptg_uchar4* out_bgra)
+{
+    if(pm.npix == 0) return PTG_OK;
+    if(j1 <= j0) return fail(PTG_E_INVALID, "empty sample range");
+    const size_t budget = size_t(1) << 30;                       // per-sample buffer <= 1 GiB
+    uint32_t chunk = uint32_t(std::max<size_t>(8, budget / (size_t(pm.npix) * sizeof(float4))));
+    chunk = std::min<uint32_t>(chunk & ~7u, j1 - j0);
+    if(chunk == 0) chunk = std::min<uint32_t>(8, j1 - j0);
+    PTG_HIP(ctx->samples.reserve(size_t(pm.npix) * chunk * sizeof(float4)));
+    PTG_HIP(ctx->acc.reserve(size_t(pm.npix) * sizeof(float4)));
+    if(ctx->counting)
+    {
+        PTG_HIP(ctx->counters.reserve(8 * sizeof(unsigned long long)));
+        PTG_HIP(hipMemsetAsync(ctx->counters.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    }
+    const DevScene sc = ctx->scene_args(cfg);
+    ctx->ev_used = 0;
+    for(uint32_t j = j0; j < j1; j += chunk)
+    {
+        const uint32_t nj = std::min(chunk, j1 - j);
+        const size_t waves = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8);
+        const size_t threads = waves * 64;
+        if(threads / kBlock + 1 > 0x7FFFFFFFull) return fail(PTG_E_RANGE, "launch too large");
+        if(ctx->timing)
+        {
+            if(ctx->ev_used == ctx->ev_start.size())
+            {
+                hipEvent_t a, b;
+                PTG_HIP(hipEventCreate(&a));
+                PTG_HIP(hipEventCreate(&b));
+                ctx->ev_start.push_back(a);
+                ctx->ev_stop.push_back(b);
+            }
+            PTG_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+        }
+        if(ctx->counting)
+            hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(threads)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj,
+                               ctx->samples.as<float4>(), ctx->counters.as<unsigned long long>());
+        else
+            hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(threads)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj,
+                               ctx->samples.as<float4>(), nullptr);
+        PTG_HIP(hipGetLastError());
+        if(ctx->timing) PTG_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used++], ctx->stream));
+        const int first = j == j0, last = j + nj >= j1;
+        hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, ctx->stream, pm, nj,
+                           ctx->samples.as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
+                           reinterpret_cast<float4*>(out_accum), reinterpret_cast<uchar4*>(out_bgra));
+        PTG_HIP(hipGetLastError());
+    }
+    if(ctx->counting)
+    {
+        unsigned long long host[8];
+        PTG_HIP(hipMemcpyAsync(host, ctx->counters.p, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
+        PTG_HIP(hipStreamSynchronize(ctx->stream));
+        for(int i = 0; i < 8; ++i) ctx->last_counters[i] = host[i];
+    }
+    return PTG_OK;
+}
+
+int pack_bvhs(ptg_context* ctx, const std::vector<BvhJob>& jobs, const ptg_bvh_node* nodes, const ptg_bvh_link* links,
+              TravRec* out)
+{
+    if(jobs.empty()) return PTG_OK;
+    PTG_HIP(ctx->jobs.reserve(jobs.size() * sizeof(BvhJob)));
+    PTG_HIP(hipMemcpyAsync(ctx->jobs.p, jobs.data(), jobs.size() * sizeof(BvhJob), hipMemcpyHostToDevice, ctx->stream));
+    uint32_t maxc = 0;
+    for(const BvhJob& j: jobs) maxc = std::max(maxc, 8 * j.count);
+    dim3 grid(std::min<uint32_t>(grid_for(maxc), 4096), uint32_t(jobs.size()));
+    hipLaunchKernelGGL(k_pack_bvh, grid, dim3(kBlock), 0, ctx->stream, nodes, links, out, ctx->jobs.as<BvhJob>());
+    PTG_HIP(hipGetLastError());
+    PTG_HIP(hipStreamSynchronize(ctx->stream));   // jobs buffer is reused
+    return PTG_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int ptg_context_create(int device, ptg_context** out)
+{
+    if(!out) return fail(PTG_E_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if(e != hipSuccess || n == 0) return fail(PTG_E_NODEVICE, "no HIP device available");
+    if(device < 0 || device >= n) return fail(PTG_E_NODEVICE, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    PTG_HIP(hipGetDeviceProperties(&prop, device));
+    if(strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(PTG_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    std::unique_ptr<ptg_context> ctx(new ptg_context());
+    ctx->device = device;
+    const char* cnt = getenv("PTG_COUNTERS");
+    ctx->counting = cnt && cnt[0] == '1';
+    PTG_HIP(hipSetDevice(device));
+    *out = ctx.release();
+    return PTG_OK;
+}
+
+void ptg_context_destroy(ptg_context* ctx)
+{
+    if(!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    delete ctx;
+}
+
+int ptg_context_set_stream(ptg_context* ctx, void* stream)
+{
+    if(int r = bind(ctx)) return r;
+    ctx->stream = static_cast<hipStream_t>(stream);
+    return PTG_OK;
+}
+
+int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_link* links, size_t node_count,
+                     const uint32_t* indices, size_t index_count, const ptg_float3* pos, const ptg_float3* normal,
+                     const ptg_float4* albedo, const ptg_float4* material, size_t vertex_count)
+{
+    if(int r = bind(ctx)) return r;
+    if(!nodes || !links || !indices || !pos || !normal || !albedo || !material || node_count == 0 || index_count % 3)
+        return fail(PTG_E_INVALID, "ptg_upload_scene: bad arguments");
+    if(node_count >= (1u << 28) / 8 || index_count >= (1u << 31) || vertex_count >= (1u << 31))
+        return fail(PTG_E_RANGE, "ptg_upload_scene: scene too large for 32-bit indexing");
+    ctx->scene_ready = ctx->frame_ready = false;
+    ctx->packed_bvh.clear();
+    ctx->packed_mesh.clear();
+    PTG_HIP(ctx->nodes.reserve(node_count * sizeof(ptg_bvh_node)));
+    PTG_HIP(ctx->links.reserve(8 * node_count * sizeof(ptg_bvh_link)));
+    PTG_HIP(ctx->indices.reserve(index_count * 4));
+    PTG_HIP(ctx->pos.reserve(vertex_count * 16));
+    PTG_HIP(ctx->normal.reserve(vertex_count * 16));
+    PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
+    PTG_HIP(ctx->material.reserve(vertex_count * 16));
+    PTG_HIP(ctx->blas_trav.reserve(8 * node_count * sizeof(TravRec)));
+    PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec)));
+    hipStream_t s = ctx->stream;
+    PTG_HIP(hipMemcpyAsync(ctx->nodes.p, nodes, node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->links.p, links, 8 * node_count * sizeof(ptg_bvh_link), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->indices.p, indices, index_count * 4, hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->pos.p, pos, vertex_count * 16, hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->normal.p, normal, vertex_count * 16, hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->albedo.p, albedo, vertex_count * 16, hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->material.p, material, vertex_count * 16, hipMemcpyHostToDevice, s));
+    PTG_HIP(hipStreamSynchronize(s));
+    ctx->static_nodes = node_count;
+    ctx->index_count = index_count;
+    ctx->vertex_count = vertex_count;
+    ctx->scene_ready = true;
+    return PTG_OK;
+}
+
+int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subframe_count,
+                     const ptg_tlas_instance* instances, size_t instance_count, const ptg_bvh_node* frame_nodes,
+                     const ptg_bvh_link* frame_links, size_t first_node, size_t frame_node_count)
+{
+    if(int r = bind(ctx)) return r;
+    if(!ctx->scene_ready) return fail(PTG_E_INVALID, "ptg_upload_frame: upload the scene first");
+    if(!subframes || !subframe_count || !instances || !instance_count || !frame_nodes || !frame_links || !frame_node_count)
+        return fail(PTG_E_INVALID, "ptg_upload_frame: bad arguments");
+    if(first_node != ctx->static_nodes)
+        return fail(PTG_E_INVALID, "ptg_upload_frame: first_node must equal the uploaded static node count");
+    if((first_node + frame_node_count) * 8 >= (1ull << 32)) return fail(PTG_E_RANGE, "ptg_upload_frame: too many nodes");
+    ctx->frame_ready = false;
+    hipStream_t s = ctx->stream;
+
+    // validate handles, pack instances, collect BLAS / mesh packing jobs
+    std::vector<InstTrav> it(instance_count);
+    std::vector<InstShade> is(instance_count);
+    std::vector<BvhJob> blas_jobs;
+    std::vector<MeshJob> mesh_jobs;
+    for(size_t i = 0; i < instance_count; ++i)
+    {
+        const ptg_tlas_instance& in = instances[i];
+        if(uint64_t(in.blas.node_offset) + in.blas.node_count > ctx->static_nodes || in.blas.node_count == 0)
+            return fail(PTG_E_RANGE, "instance " + std::to_string(i) + ": BLAS outside the static nodes");
+        if(uint64_t(in.m.index_offset) + 3ull * in.m.triangle_count > ctx->index_count || in.m.index_offset % 3 ||
+           uint64_t(in.m.base_vertex_offset) + in.m.vertex_count > ctx->vertex_count)
+            return fail(PTG_E_RANGE, "instance " + std::to_string(i) + ": mesh outside the uploaded buffers");
+        for(int k = 0; k < 4; ++k)
+        {
+            it[i].m[k * 3 + 0] = in.inv_transform.r[k].x;
+            it[i].m[k * 3 + 1] = in.inv_transform.r[k].y;
+            it[i].m[k * 3 + 2] = in.inv_transform.r[k].z;
+        }
+        it[i].blas_count = in.blas.node_count;
+        it[i].blas_offset = in.blas.node_offset;
+        it[i].tri_base = in.m.index_offset / 3;
+        it[i].pad = 0;
+        for(int k = 0; k < 3; ++k)
+        {
+            is[i].rot[k * 3 + 0] = in.transform.r[k].x;
+            is[i].rot[k * 3 + 1] = in.transform.r[k].y;
+            is[i].rot[k * 3 + 2] = in.transform.r[k].z;
+        }
+        is[i].index_offset = in.m.index_offset;
+        is[i].base_vertex_offset = in.m.base_vertex_offset;
+        std::fill(is[i].pad, is[i].pad + 5, 0u);
+        if(ctx->packed_bvh.insert(in.blas.node_offset).second)
+            blas_jobs.push_back(BvhJob{in.blas.node_offset, in.blas.node_offset * 8, in.blas.node_count,
+                                       in.blas.node_offset * 8});
+        if(ctx->packed_mesh.insert(in.m.index_offset).second)
+            mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
+    }
+    std::vector<BvhJob> tlas_jobs;
+    for(size_t i = 0; i < subframe_count; ++i)
+    {
+        const ptg_bvh& t = subframes[i].tlas;
+        if(t.node_offset < first_node || uint64_t(t.node_offset) + t.node_count > first_node + frame_node_count ||
+           t.node_count == 0)
+            return fail(PTG_E_RANGE, "subframe " + std::to_string(i) + ": TLAS outside the frame nodes");
+        const uint32_t rel = uint32_t(t.node_offset - first_node);
+        tlas_jobs.push_back(BvhJob{rel, rel * 8, t.node_count, rel * 8});
+        // every TLAS leaf must name a valid instance
+    }
+    for(size_t k = 0; k < 8 * frame_node_count; ++k)
+    {
+        const uint32_t a = frame_links[k].accept;
+        if((a & 0x80000000u) && (a & 0x7FFFFFFFu) >= instance_count)
+            return fail(PTG_E_RANGE, "TLAS leaf names instance " + std::to_string(a & 0x7FFFFFFFu));
+    }
+
+    PTG_HIP(ctx->inst_trav.reserve(instance_count * sizeof(InstTrav)));
+    PTG_HIP(ctx->inst_shade.reserve(instance_count * sizeof(InstShade)));
+    PTG_HIP(ctx->subframes.reserve(subframe_count * sizeof(ptg_subframe)));
+    PTG_HIP(ctx->frame_nodes.reserve(frame_node_count * sizeof(ptg_bvh_node)));
+    PTG_HIP(ctx->frame_links.reserve(8 * frame_node_count * sizeof(ptg_bvh_link)));
+    PTG_HIP(ctx->tlas_trav.reserve(8 * frame_node_count * sizeof(TravRec)));
+    PTG_HIP(hipMemcpyAsync(ctx->inst_trav.p, it.data(), instance_count * sizeof(InstTrav), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->inst_shade.p, is.data(), instance_count * sizeof(InstShade), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->subframes.p, subframes, subframe_count * sizeof(ptg_subframe), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->frame_nodes.p, frame_nodes, frame_node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(ctx->frame_links.p, frame_links, 8 * frame_node_count * sizeof(ptg_bvh_link),
+                           hipMemcpyHostToDevice, s));
+    if(int r = pack_bvhs(ctx, blas_jobs, ctx->nodes.as<ptg_bvh_node>(), ctx->links.as<ptg_bvh_link>(),
+                         ctx->blas_trav.as<TravRec>()))
+        return r;
+    if(int r = pack_bvhs(ctx, tlas_jobs, ctx->frame_nodes.as<ptg_bvh_node>(), ctx->frame_links.as<ptg_bvh_link>(),
+                         ctx->tlas_trav.as<TravRec>()))
+        return r;
+    if(!mesh_jobs.empty())
+    {
+        PTG_HIP(ctx->jobs.reserve(mesh_jobs.size() * sizeof(MeshJob)));
+        PTG_HIP(hipMemcpyAsync(ctx->jobs.p, mesh_jobs.data(), mesh_jobs.size() * sizeof(MeshJob), hipMemcpyHostToDevice, s));
+        uint32_t maxt = 0;
+        for(const MeshJob& j: mesh_jobs) maxt = std::max(maxt, j.triangle_count);
+        dim3 grid(std::min<uint32_t>(grid_for(maxt), 4096), uint32_t(mesh_jobs.size()));
+        hipLaunchKernelGGL(k_pack_tris, grid, dim3(kBlock), 0, s, ctx->indices.as<uint32_t>(), ctx->pos.as<float4>(),
+                           ctx->tris.as<TriRec>(), ctx->jobs.as<MeshJob>());
+        PTG_HIP(hipGetLastError());
+    }
+    PTG_HIP(hipStreamSynchronize(s));
+    ctx->first_frame_node = first_node;
+    ctx->frame_node_count = frame_node_count;
+    ctx->subframe_count = subframe_count;
+    ctx->instance_count = instance_count;
+    ctx->host_subframes.assign(subframes, subframes + subframe_count);
+    ctx->frame_ready = true;
+    return PTG_OK;
+}
+
+int ptg_upload_from_scene(ptg_context* ctx, const ptg_scene* scene, int include_static)
+{
+    ptg_scene_view v;
+    if(int r = ptg_scene_view_get(scene, &v)) return r;
+    if(include_static)
+        if(int r = ptg_upload_scene(ctx, v.nodes, v.links, v.static_node_count, v.indices, v.index_count, v.pos, v.normal,
+                                    v.albedo, v.material, v.vertex_count))
+            return r;
+    return ptg_upload_frame(ctx, v.subframes, v.subframe_count, v.instances, v.instance_count, v.nodes + v.static_node_count,
+                            v.links + 8 * v.static_node_count, v.static_node_count, v.node_count - v.static_node_count);
+}
+
+int ptg_render(ptg_context* ctx, const ptg_render_config* cfg, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+               uint32_t sample_begin, uint32_t sample_end, ptg_float4* out_accum, ptg_uchar4* out_bgra)
+{
+    if(int r = bind(ctx)) return r;
+    if(int r = check_cfg(ctx, cfg, sample_end)) return r;
+    if(uint64_t(x0) + w > cfg->width || uint64_t(y0) + h > cfg->height) return fail(PTG_E_RANGE, "rectangle outside the image");
+    PixelMap pm{};
+    pm.tiles = 0;
+    pm.x0 = x0; pm.y0 = y0; pm.w = w; pm.h = h;
+    pm.img_w = cfg->width; pm.img_h = cfg->height;
+    pm.npix = w * h;
+    return render_map(ctx, cfg, pm, sample_begin, sample_end, out_accum, out_bgra);
+}
+
+static int tile_map(const ptg_render_config* cfg, uint32_t tw, uint32_t th, uint32_t first, uint32_t stride,
+                    uint32_t count, PixelMap& pm)
+{
+    if(tw == 0 || th == 0 || stride == 0) return fail(PTG_E_INVALID, "bad tile geometry");
+    const uint32_t tx = (cfg->width + tw - 1) / tw, ty = (cfg->height + th - 1) / th;
+    if(count && uint64_t(first) + uint64_t(count - 1) * stride >= uint64_t(tx) * ty)
+        return fail(PTG_E_RANGE, "tile index beyond the image");
+    if(uint64_t(count) * tw * th >= (1ull << 31)) return fail(PTG_E_RANGE, "too many tile pixels");
+    pm = PixelMap{};
+    pm.tiles = 1;
+    pm.tw = tw; pm.th = th; pm.tiles_x = tx; pm.first = first; pm.stride = stride;
+    pm.img_w = cfg->width; pm.img_h = cfg->height;
+    pm.npix = count * tw * th;
+    return PTG_OK;
+}
+
+int ptg_render_tiles(ptg_context* ctx, const ptg_render_config* cfg, uint32_t tile_w, uint32_t tile_h, uint32_t first_tile,
+                     uint32_t tile_stride, uint32_t tile_count, ptg_float4* out_accum, ptg_uchar4* out_bgra)
+{
+    if(int r = bind(ctx)) return r;
+    if(int r = check_cfg(ctx, cfg, cfg ? cfg->samples_per_pixel : 0)) return r;
+    PixelMap pm;
+    if(int r = tile_map(cfg, tile_w, tile_h, first_tile, tile_stride, tile_count, pm)) return r;
+    return render_map(ctx, cfg, pm, 0, cfg->samples_per_pixel, out_accum, out_bgra);
+}
+
+int ptg_scatter_tiles(ptg_context* ctx, const ptg_render_config* cfg, uint32_t tile_w, uint32_t tile_h,
+                      uint32_t first_tile, uint32_t tile_stride, uint32_t tile_count, const ptg_uchar4* tiles,
+                      ptg_uchar4* image)
+{
+    if(int r = bind(ctx)) return r;
+    if(!cfg || !tiles || !image) return fail(PTG_E_INVALID, "ptg_scatter_tiles: bad arguments");
+    PixelMap pm;
+    if(int r = tile_map(cfg, tile_w, tile_h, first_tile, tile_stride, tile_count, pm)) return r;
+    if(pm.npix == 0) return PTG_OK;
+    hipLaunchKernelGGL(k_scatter_tiles, dim3(grid_for(pm.npix)), dim3(kBlock), 0, ctx->stream, pm,
+                       reinterpret_cast<const uchar4*>(tiles), reinterpret_cast<uchar4*>(image));
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
+int ptg_path_trace_samples(ptg_context* ctx, const ptg_render_config* cfg, size_t n, const ptg_uint2* xy,
+                           const int32_t* sample_index, ptg_float4* out)
+{
+    if(int r = bind(ctx)) return r;
+    if(int r = check_cfg(ctx, cfg, 0)) return r;
+    if(!n) return PTG_OK;
+    if(!xy || !sample_index || !out || n >= (1u << 30)) return fail(PTG_E_INVALID, "ptg_path_trace_samples: bad arguments");
+    int32_t jmax = 0;
+    for(size_t i = 0; i < n; ++i)
+    {
+        jmax = std::max(jmax, sample_index[i]);
+        if(xy[i].x >= cfg->width || xy[i].y >= cfg->height) return fail(PTG_E_RANGE, "pixel outside the image");
+    }
+    if(uint64_t(jmax) / cfg->samples_per_motion_blur_step >= ctx->subframe_count)
+        return fail(PTG_E_RANGE, "sample index beyond the frame's subframes");
+    PTG_HIP(ctx->tmp_a.reserve(n * sizeof(uint2)));
+    PTG_HIP(ctx->tmp_b.reserve(n * sizeof(int32_t)));
+    PTG_HIP(ctx->tmp_c.reserve(n * sizeof(float4)));
+    PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, xy, n * sizeof(uint2), hipMemcpyHostToDevice, ctx->stream));
+    PTG_HIP(hipMemcpyAsync(ctx->tmp_b.p, sample_index, n * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_sample_list, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(cfg), uint32_t(n),
+                       ctx->tmp_a.as<uint2>(), ctx->tmp_b.as<int32_t>(), ctx->tmp_c.as<float4>());
+    PTG_HIP(hipGetLastError());
+    PTG_HIP(hipMemcpyAsync(out, ctx->tmp_c.p, n * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    PTG_HIP(hipStreamSynchronize(ctx->stream));
+    return PTG_OK;
+}
+
+int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4* out)
+{
+    if(int r = bind(ctx)) return r;
+    if(!n) return PTG_OK;
+    if(!color || !out || n >= (1u << 30)) return fail(PTG_E_INVALID, "ptg_tonemap: bad arguments");
+    PTG_HIP(ctx->tmp_c.reserve(n * sizeof(float4)));
+    PTG_HIP(ctx->tmp_a.reserve(n * sizeof(uchar4)));
+    PTG_HIP(hipMemcpyAsync(ctx->tmp_c.p, color, n * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_tonemap, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, uint32_t(n), ctx->tmp_c.as<float4>(),
+                       ctx->tmp_a.as<uchar4>());
+    PTG_HIP(hipGetLastError());
+    PTG_HIP(hipMemcpyAsync(out, ctx->tmp_a.p, n * sizeof(uchar4), hipMemcpyDeviceToHost, ctx->stream));
+    PTG_HIP(hipStreamSynchronize(ctx->stream));
+    return PTG_OK;
+}
+
+int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* rays, uint32_t* hits)
+{
+    if(int r = bind(ctx)) return r;
+    if(!ctx->scene_ready || !ctx->frame_ready) return fail(PTG_E_INVALID, "scene/frame not uploaded");
+    if(subframe >= ctx->subframe_count) return fail(PTG_E_RANGE, "subframe out of range");
+    if(!n) return PTG_OK;
+    if(!rays || !hits || n >= (1u << 28)) return fail(PTG_E_INVALID, "ptg_trace_rays: bad arguments");
+    PTG_HIP(ctx->tmp_a.reserve(n * 32));
+    PTG_HIP(ctx->tmp_b.reserve(n * 32));
+    PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, rays, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    const ptg_bvh t = ctx->host_subframes[subframe].tlas;
+    hipLaunchKernelGGL(k_rays, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(nullptr), t.node_count,
+                       t.node_offset, uint32_t(n), ctx->tmp_a.as<float>(), ctx->tmp_b.as<uint32_t>());
+    PTG_HIP(hipGetLastError());
+    PTG_HIP(hipMemcpyAsync(hits, ctx->tmp_b.p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+    PTG_HIP(hipStreamSynchronize(ctx->stream));
+    return PTG_OK;
+}
+
+int ptg_last_counters(ptg_context* ctx, uint64_t out[8])
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_counters: bad arguments");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable or PTG_COUNTERS=1)");
+    memcpy(out, ctx->last_counters, sizeof(ctx->last_counters));
+    return PTG_OK;
+}
+
+int ptg_counters_enable(ptg_context* ctx, int enable)
+{
+    if(!ctx) return fail(PTG_E_INVALID, "null context");
+    ctx->counting = enable != 0;
+    return PTG_OK;
+}
+
+int ptg_timing_enable(ptg_context* ctx, int enable)
+{
+    if(!ctx) return fail(PTG_E_INVALID, "null context");
+    ctx->timing = enable != 0;
+    return PTG_OK;
+}
+
+int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches)
+{
+    if(int r = bind(ctx)) return r;
+    if(!trace_ms || !launches) return fail(PTG_E_INVALID, "ptg_last_timing: bad arguments");
+    double total = 0;
+    for(size_t i = 0; i < ctx->ev_used; ++i)
+    {
+        PTG_HIP(hipEventSynchronize(ctx->ev_stop[i]));
+        float ms = 0;
+        PTG_HIP(hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
+        total += ms;
+    }
+    *trace_ms = total;
+    *launches = uint32_t(ctx->ev_used);
+    return PTG_OK;
+}
+
+int ptg_synchronize(ptg_context* ctx)
+{
+    if(int r = bind(ctx)) return r;
+    PTG_HIP(hipStreamSynchronize(ctx->stream));
+    return PTG_OK;
+}
+
+int ptg_device_alloc(ptg_context* ctx, size_t bytes, void** out)
+{
+    if(int r = bind(ctx)) return r;
+    if(!out) return fail(PTG_E_INVALID, "null out");
+    PTG_HIP(hipMalloc(out, bytes));
+    return PTG_OK;
+}
+
+int ptg_device_free(ptg_context* ctx, void* p)
+{
+    if(int r = bind(ctx)) return r;
+    PTG_HIP(hipFree(p));
+    return PTG_OK;
+}
+
+int ptg_memcpy_d2h(ptg_context* ctx, void* dst, const void* src, size_t bytes)
+{
+    if(int r = bind(ctx)) return r;
+    PTG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PTG_HIP(hipStreamSynchronize(ctx->stream));
+    return PTG_OK;
+}
+
+} // extern "C"

@@ -103,7 +103,10 @@ def lib():
         "ptg_path_trace_samples": (I, [P, P, SZ, P, P, P]),
         "ptg_tonemap": (I, [P, SZ, P, P]),
         "ptg_trace_rays": (I, [P, U32, SZ, P, P]),
+        "ptg_counters_enable": (I, [P, I]),
         "ptg_last_counters": (I, [P, P]),
+        "ptg_timing_enable": (I, [P, I]),
+        "ptg_last_timing": (I, [P, C.POINTER(C.c_double), C.POINTER(U32)]),
         "ptg_synchronize": (I, [P]),
         "ptg_device_alloc": (I, [P, SZ, C.POINTER(P)]),
         "ptg_device_free": (I, [P, P]),

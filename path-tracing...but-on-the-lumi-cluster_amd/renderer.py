@@ -1,0 +1,163 @@
+"""GPU renderer: the MI355X replacement of the reference's baseline_render.
+
+``GpuRenderer`` owns one ``ptg_context`` (one GPU).  The reference drives its
+hot path as
+
+    load_scene(); setup_animation_frame(s, f); baseline_render(s, image)
+    (main.cc:67, :82, :88)
+
+and the same flow here is
+
+    scene = Scene(assets, cfg); scene.setup_frame(f)
+    r = GpuRenderer(device); r.upload(scene); img = r.render(cfg)
+
+Everything below the C ABI runs in HIP kernels; this class only moves
+pointers.  Device outputs are torch tensors (torch is used for device memory,
+streams and torch.distributed only).  There is no CPU fallback: without a
+gfx950 device the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import native as N
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class GpuRenderer:
+    def __init__(self, device: int = 0, stream=None):
+        import torch  # noqa: F401  (device memory + streams)
+        self._ctx = C.c_void_p()
+        N.check(N.lib().ptg_context_create(device, C.byref(self._ctx)), "ptg_context_create")
+        self.device = device
+        self.scene_uploaded = False
+        if stream is not None:
+            self.set_stream(stream)
+
+    # -- streams ---------------------------------------------------------
+    def set_stream(self, stream):
+        """Launch on a torch.cuda.Stream (or raw hipStream_t int)."""
+        handle = getattr(stream, "cuda_stream", stream)
+        N.check(N.lib().ptg_context_set_stream(self._ctx, C.c_void_p(handle)), "ptg_context_set_stream")
+
+    def synchronize(self):
+        N.check(N.lib().ptg_synchronize(self._ctx), "ptg_synchronize")
+
+    # -- uploads ---------------------------------------------------------
+    def upload(self, scene: N.Scene, include_static=None):
+        """upload_scene (once) + upload_frame (every frame) from a host Scene."""
+        if include_static is None:
+            include_static = not self.scene_uploaded
+        N.check(N.lib().ptg_upload_from_scene(self._ctx, scene.handle, 1 if include_static else 0),
+                "ptg_upload_from_scene")
+        self.scene_uploaded = True
+
+    def upload_arrays(self, arrays: dict, include_static=True):
+        """Upload reference-layout numpy arrays (the keys of Scene.view())."""
+        L = N.lib()
+        a = {k: (np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v) for k, v in arrays.items()}
+        sn = int(a["static_node_count"])
+        if include_static:
+            N.check(L.ptg_upload_scene(self._ctx, a["nodes"].ctypes.data, a["links"].ctypes.data, sn,
+                                       a["indices"].ctypes.data, a["indices"].size, a["pos"].ctypes.data,
+                                       a["normal"].ctypes.data, a["albedo"].ctypes.data, a["material"].ctypes.data,
+                                       a["pos"].shape[0]), "ptg_upload_scene")
+        nodes = a["nodes"][sn:]
+        links = a["links"][8 * sn:]
+        N.check(L.ptg_upload_frame(self._ctx, a["subframes"].ctypes.data, a["subframes"].size,
+                                   a["instances"].ctypes.data, a["instances"].size,
+                                   np.ascontiguousarray(nodes).ctypes.data, np.ascontiguousarray(links).ctypes.data,
+                                   sn, nodes.size), "ptg_upload_frame")
+        self.scene_uploaded = True
+
+    # -- rendering -------------------------------------------------------
+    def render(self, cfg: N.RenderConfig, rect=None, samples=None, out_bgra=None, out_accum=None,
+               want_accum=False):
+        """baseline_render over `rect` = (x0, y0, w, h) (default: the whole
+        image) and sample range `samples` = (begin, end) (default: all).
+        Returns (bgra uint8 [h, w, 4], accum float32 [h, w, 4] or None) as
+        torch tensors on this GPU.  Asynchronous on the context stream."""
+        import torch
+        x0, y0, w, h = rect if rect is not None else (0, 0, cfg.width, cfg.height)
+        j0, j1 = samples if samples is not None else (0, cfg.samples_per_pixel)
+        dev = torch.device("cuda", self.device)
+        if out_bgra is None:
+            out_bgra = torch.empty((h, w, 4), dtype=torch.uint8, device=dev)
+        if out_accum is None and want_accum:
+            out_accum = torch.empty((h, w, 4), dtype=torch.float32, device=dev)
+        N.check(N.lib().ptg_render(self._ctx, C.byref(cfg), x0, y0, w, h, j0, j1, _ptr(out_accum), _ptr(out_bgra)),
+                "ptg_render")
+        return out_bgra, out_accum
+
+    def render_tiles(self, cfg: N.RenderConfig, tile_w, tile_h, first, stride, count, out_bgra=None,
+                     out_accum=None):
+        """Render an interleaved tile set densely (multi-GPU sharding unit)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        n = count * tile_w * tile_h
+        if out_bgra is None:
+            out_bgra = torch.empty((n, 4), dtype=torch.uint8, device=dev)
+        N.check(N.lib().ptg_render_tiles(self._ctx, C.byref(cfg), tile_w, tile_h, first, stride, count,
+                                         _ptr(out_accum), _ptr(out_bgra)), "ptg_render_tiles")
+        return out_bgra, out_accum
+
+    def scatter_tiles(self, cfg, tile_w, tile_h, first, stride, count, tiles_bgra, image_bgra):
+        N.check(N.lib().ptg_scatter_tiles(self._ctx, C.byref(cfg), tile_w, tile_h, first, stride, count,
+                                          _ptr(tiles_bgra), _ptr(image_bgra)), "ptg_scatter_tiles")
+
+    # -- per-sample / per-ray entry points (parity) -------------------------
+    def path_trace_samples(self, cfg, xy: np.ndarray, sample_index: np.ndarray) -> np.ndarray:
+        xy = np.ascontiguousarray(xy, dtype=np.uint32).reshape(-1, 2)
+        js = np.ascontiguousarray(sample_index, dtype=np.int32).reshape(-1)
+        out = np.zeros((len(js), 4), np.float32)
+        N.check(N.lib().ptg_path_trace_samples(self._ctx, C.byref(cfg), len(js), xy.ctypes.data, js.ctypes.data,
+                                               out.ctypes.data), "ptg_path_trace_samples")
+        return out
+
+    def trace_rays(self, subframe: int, rays: np.ndarray) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros((len(rays), 8), np.uint32)
+        N.check(N.lib().ptg_trace_rays(self._ctx, subframe, len(rays), rays.ctypes.data, hits.ctypes.data),
+                "ptg_trace_rays")
+        return hits
+
+    def tonemap(self, colors: np.ndarray) -> np.ndarray:
+        c = np.zeros((colors.shape[0], 4), np.float32)
+        c[:, :colors.shape[1]] = colors[:, :4] if colors.shape[1] >= 4 else colors
+        c = np.ascontiguousarray(c)
+        out = np.zeros((len(c), 4), np.uint8)
+        N.check(N.lib().ptg_tonemap(self._ctx, len(c), c.ctypes.data, out.ctypes.data), "ptg_tonemap")
+        return out
+
+    def enable_timing(self, on=True):
+        N.check(N.lib().ptg_timing_enable(self._ctx, 1 if on else 0), "ptg_timing_enable")
+
+    def last_timing(self):
+        """(summed k_trace device ms, launch count) of the last render call."""
+        ms, n = C.c_double(), C.c_uint32()
+        N.check(N.lib().ptg_last_timing(self._ctx, C.byref(ms), C.byref(n)), "ptg_last_timing")
+        return ms.value, n.value
+
+    def enable_counters(self, on=True):
+        N.check(N.lib().ptg_counters_enable(self._ctx, 1 if on else 0), "ptg_counters_enable")
+
+    def counters(self):
+        out = np.zeros(8, np.uint64)
+        N.check(N.lib().ptg_last_counters(self._ctx, out.ctypes.data), "ptg_last_counters")
+        return out
+
+    def close(self):
+        if self._ctx:
+            N.lib().ptg_context_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
