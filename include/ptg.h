@@ -230,6 +230,8 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
  * [4] ray queries, [5] closest-hit shades. */
 int ptg_counters_enable(ptg_context* ctx, int enable);
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
+/* Counters split by kernel kind (same kinds as ptg_last_kernel_times). */
+int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
 
 /* Per-launch timing of the path-tracing kernel (k_trace), measured with HIP
  * events on the context's stream.  After enabling, each ptg_render* call
@@ -237,6 +239,15 @@ int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
  * count (waits for the last launch). */
 int ptg_timing_enable(ptg_context* ctx, int enable);
 int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches);
+/* The same per kernel kind: [0] megakernel, [1] extend (closest-hit walk),
+ * [2] shadow (any-hit walk), [3] shade, [4] camera, [5] accumulate. */
+int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8]);
+
+/* Execution strategy of ptg_render*: 0 = wavefront pipeline (default:
+ * camera / extend / shadow / shade kernels over compacted path queues),
+ * 1 = megakernel (one work-item runs a whole path).  Both produce identical
+ * bits; PTG_PIPELINE=megakernel selects 1 at context creation. */
+int ptg_set_pipeline(ptg_context* ctx, int pipeline);
 
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);

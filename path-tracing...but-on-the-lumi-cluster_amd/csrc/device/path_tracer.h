@@ -51,50 +51,71 @@ PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
     hi = q[1];
 }
 
-// One ray query.  ANY = true: trace_shadow_ray (path_tracer.hh:415-427),
-// i.e. the first accepted candidate ends the walk.  ANY = false: closest hit
-// (proceed/confirm loop of trace_ray, path_tracer.hh:342-349).
-template<bool ANY, bool COUNT>
-PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, f3 o, f3 d, float tmin, float tmax,
-                 Hit& best, Counters& cnt)
-{
-    if(COUNT) cnt.queries++;
-    const f3 inv_w = V3(rcp_or_big(d.x), rcp_or_big(d.y), rcp_or_big(d.z));
-    const uint32_t tlas_base = tlas_offset * 8 + octant(d) * tlas_count - sc.tlas_link_base;
+// One ray query, resumable: the walk state of ray_query (ray_query.hh:66-109)
+// for both levels, advanced one BVH step at a time by step().  ANY = true is
+// trace_shadow_ray (path_tracer.hh:415-427): the first accepted candidate
+// ends the walk.  ANY = false is the proceed/confirm loop of trace_ray
+// (path_tracer.hh:342-349): every accepted candidate is confirmed and
+// shortens tmax.  The flat step (TLAS node, BLAS node, BLAS entry, triangle
+// test or BLAS exit) keeps the lanes of a wave stepping together whatever
+// level each one is in.
+struct Walker {
+    f3 o, d, inv_w;            // world ray and its reciprocal direction
+    float tmin, tmax;
+    uint32_t tlas_base, tlas_count;
+    f3 org, inv;               // active level: ray origin / 1/dir in that level's space
+    uint32_t base, node, count;
+    uint32_t tlas_resume;      // TLAS node to continue with after the BLAS
+    f3 S;                      // BLAS: shear constants of ray_triangle_intersection_preprocess
+    int axis;                  // BLAS: dominant axis, -1 while in the TLAS (blas_axis)
+    uint32_t tri_base, inst;
+    Hit best;
 
-    // active level state
-    const TravRec* recs = sc.tlas_trav + tlas_base;
-    f3 org = o, inv = inv_w;
-    uint32_t node = 0, count = tlas_count;
-    bool in_blas = false;
-    uint32_t tlas_resume = 0;     // TLAS node to continue with after the BLAS
-    // BLAS level extras
-    f3 S = V3(0, 0, 0);
-    int axis = 2;
-    uint32_t tri_base = 0, inst = 0xFFFFFFFFu;
+    PTG_D void init(const DevScene& sc, uint32_t tc, uint32_t to, f3 ro, f3 rd, float t0, float t1)
+    {
+        o = ro;
+        d = rd;
+        inv_w = V3(rcp_or_big(rd.x), rcp_or_big(rd.y), rcp_or_big(rd.z));
+        tmin = t0;
+        tmax = t1;
+        tlas_count = tc;
+        tlas_base = to * 8 + octant(rd) * tc - sc.tlas_link_base;
+        org = o;
+        inv = inv_w;
+        base = tlas_base;
+        node = 0;
+        count = tc;
+        tlas_resume = 0;
+        S = V3(0, 0, 0);
+        axis = -1;
+        tri_base = 0;
+        inst = 0xFFFFFFFFu;
+        best.thit = -1.0f;
+        best.bx = best.by = best.bz = 0.0f;
+        best.instance_id = 0xFFFFFFFFu;
+        best.primitive_id = 0;
+        best.back_face = false;
+    }
 
-    best.thit = -1.0f;
-    best.bx = best.by = best.bz = 0.0f;
-    best.instance_id = 0xFFFFFFFFu;
-    best.primitive_id = 0;
-    best.back_face = false;
-
-    for(;;)
+    // One step.  Returns 0 while the walk goes on, 1 when it has ended, 2 (ANY
+    // only) when an occluder was found.
+    template<bool ANY, bool COUNT>
+    PTG_D int step(const DevScene& sc, Counters& cnt)
     {
         if(node >= count)
         {
-            if(!in_blas) break;
+            if(axis < 0) return 1;
             // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
-            in_blas = false;
-            recs = sc.tlas_trav + tlas_base;
+            axis = -1;
+            base = tlas_base;
             org = o;
             inv = inv_w;
             node = tlas_resume;
             count = tlas_count;
-            continue;
+            return 0;
         }
         float4 lo, hi;
-        load_trav(recs + node, lo, hi);
+        load_trav((axis < 0 ? sc.tlas_trav : sc.blas_trav) + base + node, lo, hi);
         if(COUNT) cnt.visits++;
         // slab test (ray_query.hh:197-207); min/max results only feed compares
         const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
@@ -103,11 +124,11 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
         const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
         const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
         const uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
-        if(!(nearv <= farv && farv > tmin && nearv < tmax)) { node = cancel; continue; }
-        if(!(accept & 0x80000000u)) { node = accept; continue; }
+        if(!(nearv <= farv && farv > tmin && nearv < tmax)) { node = cancel; return 0; }
+        if(!(accept & 0x80000000u)) { node = accept; return 0; }
         node = cancel;
         const uint32_t leaf = accept & 0x7FFFFFFFu;
-        if(!in_blas)
+        if(axis < 0)
         {
             // ray_query_enter_blas (ray_query.hh:153-182)
             if(COUNT) cnt.blas_entries++;
@@ -115,9 +136,9 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
             const float4 a = ip[0], b = ip[1], c = ip[2], e = ip[3];
             // a = M0.xyz M1.x | b = M1.yz M2.xy | c = M2.z M3.xyz | e = blas count, offset, tri_base
             const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(a.w, b.x, b.y), M2 = V3(b.z, b.w, c.x), M3 = V3(c.y, c.z, c.w);
-            const f3 bo = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
-                             M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
-                             M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
+            org = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
+                     M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
+                     M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
             const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
                              M0.y * d.x + M1.y * d.y + M2.y * d.z,
                              M0.z * d.x + M1.z * d.y + M2.z * d.z);
@@ -125,10 +146,8 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
             tri_base = __float_as_uint(e.z);
             inst = leaf;
             tlas_resume = node;
-            in_blas = true;
-            org = bo;
             inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
-            recs = sc.blas_trav + (boffset * 8 + octant(bd) * bcount);
+            base = boffset * 8 + octant(bd) * bcount;
             count = bcount;
             node = 0;
             // ray_triangle_intersection_preprocess (math.hh:340-356)
@@ -139,7 +158,7 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
             else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
             const float k = 1.0f / rd.z;
             S = V3(rd.x * k, rd.y * k, 1.0f * k);
-            continue;
+            return 0;
         }
         // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246, math.hh:358-401)
         if(COUNT) cnt.tri_tests++;
@@ -163,7 +182,7 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
                           (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f));
         if(hit && t < tmax && t > tmin)
         {
-            if(ANY) return true;
+            if(ANY) return 2;
             // ray_query_confirm (ray_query.hh:280-290)
             best.bx = u;
             best.by = v;
@@ -174,8 +193,22 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
             best.back_face = back;
             tmax = t;
         }
+        return 0;
     }
-    return ANY ? false : best.thit >= 0.0f;
+};
+
+// A whole query on one lane.  Returns whether the ray hit (ANY: occluded).
+template<bool ANY, bool COUNT>
+PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, f3 o, f3 d, float tmin, float tmax,
+                 Hit& best, Counters& cnt)
+{
+    if(COUNT) cnt.queries++;
+    Walker w;
+    w.init(sc, tlas_count, tlas_offset, o, d, tmin, tmax);
+    int r;
+    while((r = w.template step<ANY, COUNT>(sc, cnt)) == 0) {}
+    best = w.best;
+    return ANY ? r == 2 : best.thit >= 0.0f;
 }
 
 struct HitInfo {
@@ -198,13 +231,11 @@ PTG_D f3 ld3(const float* base, uint32_t i)
 }
 PTG_D float4 ld4(const float* base, uint32_t i) { return reinterpret_cast<const float4*>(base)[i]; }
 
-// trace_ray (path_tracer.hh:340-412)
+// The shading half of trace_ray (path_tracer.hh:351-411): turn the closest
+// hit of the ray (origin, dir) into a hit_info.
 template<bool COUNT>
-PTG_D HitInfo trace_ray(const DevScene& sc, uint32_t tc, uint32_t to, const Light& L, f3 origin, f3 dir, float tmin,
-                        Counters& cnt)
+PTG_D HitInfo hit_info(const DevScene& sc, const Light& L, f3 origin, f3 dir, const Hit& h, Counters& cnt)
 {
-    Hit h;
-    trace<false, COUNT>(sc, tc, to, origin, dir, tmin, 1e9f, h, cnt);
     HitInfo hi;
     hi.thit = h.thit;
     hi.nee_pdf = 0;
@@ -245,6 +276,16 @@ PTG_D HitInfo trace_ray(const DevScene& sc, uint32_t tc, uint32_t to, const Ligh
     hi.tbn = tangent_space(n);
     hi.roughness = mx * mx;
     return hi;
+}
+
+// trace_ray (path_tracer.hh:340-412)
+template<bool COUNT>
+PTG_D HitInfo trace_ray(const DevScene& sc, uint32_t tc, uint32_t to, const Light& L, f3 origin, f3 dir, float tmin,
+                        Counters& cnt)
+{
+    Hit h;
+    trace<false, COUNT>(sc, tc, to, origin, dir, tmin, 1e9f, h, cnt);
+    return hit_info<COUNT>(sc, L, origin, dir, h, cnt);
 }
 
 // ---- samplers (path_tracer.hh:12-83) ----
@@ -476,6 +517,9 @@ PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     float tmin = 0, atmax = 0;
+#ifdef PTG_ABLATE_ATMO
+    return V3(1.0f, 1.0f, 1.0f);
+#endif
     if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return V3(1.0f, 1.0f, 1.0f);
     tmin = (float)gmax_d((double)tmin, 0.0);
     tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
@@ -502,6 +546,9 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     attenuation = V3(1.0f, 1.0f, 1.0f);
     in_scatter = V3(0.0f, 0.0f, 0.0f);
+#ifdef PTG_ABLATE_ATMO
+    return;
+#endif
     if(tmax > 0 && tmax < 1e3f) return;
     float tmin = 0, atmax = 0;
     if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return;
@@ -550,24 +597,47 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
     in_scatter = ((((ray_sum * R) * rayleigh_phase) + ((mie_sum * Mk) * mie_phase)) * L.color) * 4.0f;
 }
 
-// nee_branch (:594-620)
+// nee_branch (:594-620), split at its shadow ray so the wavefront pipeline
+// can trace that ray in a separate kernel:
+//   nee_prepare: the NEE random draw, the sun-cone direction, the BSDF value
+//                and MIS weight; returns false when the colour is zero (the
+//                reference then returns 0 without tracing);
+//   nee_finish:  for an unoccluded shadow ray, the transmittance along it and
+//                the MIS division.
+struct NeeCandidate {
+    f3 color, dir;
+    float mis_pdf, jitter;
+};
+
+PTG_D bool nee_prepare(u4& seed, const Light& L, const HitInfo& info, const Material& M, f3 tview, NeeCandidate& c)
+{
+    const f4 u = uniform4(seed);
+    c.dir = sample_cone(L.dir, L.cos, f2{u.x, u.y});
+    c.jitter = u.w;
+    const float nee_pdf = 1.0f / (2.0f * PI_F * (1.0f - L.cos));
+    float bsdf_pdf = 0;
+    const f3 b = bsdf_eval(mul_v3m3(c.dir, info.tbn), tview, M, bsdf_pdf);
+    c.color = (b * nee_pdf) * L.color;
+    c.mis_pdf = 1.0f;
+    if(L.cos < 1.0f) c.mis_pdf = (nee_pdf * nee_pdf + bsdf_pdf * bsdf_pdf) / nee_pdf;
+    return !(c.color.x == 0 && c.color.y == 0 && c.color.z == 0);
+}
+
+PTG_D f3 nee_finish(const NeeCandidate& c, f3 pos)
+{
+    const f3 color = c.color * atmosphere_attenuation(c.jitter, pos, c.dir, MAX_RAY_DIST);
+    return color / c.mis_pdf;
+}
+
 template<bool COUNT>
 PTG_D f3 nee_branch(const DevScene& sc, uint32_t tc, uint32_t to, u4& seed, const Light& L, const HitInfo& info,
                     const Material& M, f3 tview, Counters& cnt)
 {
-    const f4 u = uniform4(seed);
-    const f3 light_dir = sample_cone(L.dir, L.cos, f2{u.x, u.y});
-    const float nee_pdf = 1.0f / (2.0f * PI_F * (1.0f - L.cos));
-    float bsdf_pdf = 0;
-    const f3 b = bsdf_eval(mul_v3m3(light_dir, info.tbn), tview, M, bsdf_pdf);
-    f3 color = (b * nee_pdf) * L.color;
-    if(color.x == 0 && color.y == 0 && color.z == 0) return V3(0, 0, 0);
+    NeeCandidate c;
+    if(!nee_prepare(seed, L, info, M, tview, c)) return V3(0, 0, 0);
     Hit unused;
-    if(trace<true, COUNT>(sc, tc, to, info.pos, light_dir, MIN_RAY_DIST, MAX_RAY_DIST, unused, cnt)) return V3(0, 0, 0);
-    float mis_pdf = 1.0f;
-    if(L.cos < 1.0f) mis_pdf = (nee_pdf * nee_pdf + bsdf_pdf * bsdf_pdf) / nee_pdf;
-    color = color * atmosphere_attenuation(u.w, info.pos, light_dir, MAX_RAY_DIST);
-    return color / mis_pdf;
+    if(trace<true, COUNT>(sc, tc, to, info.pos, c.dir, MIN_RAY_DIST, MAX_RAY_DIST, unused, cnt)) return V3(0, 0, 0);
+    return nee_finish(c, info.pos);
 }
 
 PTG_D float rd_f(const uint8_t* p, uint32_t off) { return *reinterpret_cast<const float*>(p + off); }
@@ -578,49 +648,91 @@ PTG_D f3 rd_f3(const uint8_t* p, uint32_t off)
     return V3(v.x, v.y, v.z);
 }
 
-// path_trace_pixel (path_tracer.hh:637-741)
-template<bool COUNT>
-PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
+// subframes[sample_index / SAMPLES_PER_MOTION_BLUR_STEP] (path_tracer.hh:655-657)
+PTG_D const uint8_t* subframe_of(const DevScene& sc, int32_t sample_index)
 {
     const uint32_t sub = sample_index < 0 ? 0u : (uint32_t)sample_index / sc.blur_step;
-    const uint8_t* sf = sc.subframes + size_t(sub) * SF_STRIDE;
-    const uint32_t tc = rd_u(sf, SF_TLAS), to = rd_u(sf, SF_TLAS + 4);
+    return sc.subframes + size_t(sub) * SF_STRIDE;
+}
+PTG_D Light light_of(const uint8_t* sf)
+{
     Light L;
     L.dir = rd_f3(sf, SF_LIGHT);
     L.color = rd_f3(sf, SF_LIGHT + 16);
     L.cos = rd_f(sf, SF_LIGHT + 32);
+    return L;
+}
 
-    u4 seed{px, py, (uint32_t)sample_index, sc.student_id};
+// Seed initialisation, film jitter and get_camera_ray (path_tracer.hh:659-671, :429-450).
+PTG_D void camera_ray(const DevScene& sc, const uint8_t* sf, uint32_t px, uint32_t py, int32_t sample_index, u4& seed,
+                      f3& ray_o, f3& ray_dir)
+{
+    seed = u4{px, py, (uint32_t)sample_index, sc.student_id};
     pcg4d(seed);
     const f4 u = uniform4(seed);
     f2 film = gaussian_disk(f2{u.x, u.y}, 0.4f);
     film.x = film.x + 0.5f;
     film.y = film.y + 0.5f;
-
-    // get_camera_ray (:429-450)
     const uint8_t* cam = sf + SF_CAM;
-    f3 ray_dir, ray_o;
+    float uvx = ((float)px + film.x) / (float)sc.width * 2.0f - 1.0f;
+    float uvy = ((float)py + film.y) / (float)sc.height * 2.0f - 1.0f;
+    uvx *= rd_f(cam, 64);
+    uvy = -uvy;
+    f2 ap{0, 0};
+    const int32_t polygon = (int32_t)rd_u(cam, 80);
+    if(polygon > 3)
     {
-        float uvx = ((float)px + film.x) / (float)sc.width * 2.0f - 1.0f;
-        float uvy = ((float)py + film.y) / (float)sc.height * 2.0f - 1.0f;
-        uvx *= rd_f(cam, 64);
-        uvy = -uvy;
-        f2 ap{0, 0};
-        const int32_t polygon = (int32_t)rd_u(cam, 80);
-        if(polygon > 3)
-        {
-            const f2 p = regular_polygon(f2{u.z, u.w}, rd_f(cam, 76), (uint32_t)polygon);
-            const float rad = rd_f(cam, 84);
-            ap = f2{p.x * rad, p.y * rad};
-        }
-        const f3 origin = V3(ap.x, ap.y, 0.0f);
-        const float ifl = rd_f(cam, 68), fd = rd_f(cam, 72);
-        f3 d = V3(uvx * ifl * fd, uvy * ifl * fd, -1.0f * fd);
-        d = normalize(d - origin);
-        const m3 ori{{rd_f3(cam, 0), rd_f3(cam, 16), rd_f3(cam, 32)}};
-        ray_dir = mul_m3v3(ori, d);
-        ray_o = mul_m3v3(ori, origin) + rd_f3(cam, 48);
+        const f2 p = regular_polygon(f2{u.z, u.w}, rd_f(cam, 76), (uint32_t)polygon);
+        const float rad = rd_f(cam, 84);
+        ap = f2{p.x * rad, p.y * rad};
     }
+    const f3 origin = V3(ap.x, ap.y, 0.0f);
+    const float ifl = rd_f(cam, 68), fd = rd_f(cam, 72);
+    f3 d = V3(uvx * ifl * fd, uvy * ifl * fd, -1.0f * fd);
+    d = normalize(d - origin);
+    const m3 ori{{rd_f3(cam, 0), rd_f3(cam, 16), rd_f3(cam, 32)}};
+    ray_dir = mul_m3v3(ori, d);
+    ray_o = mul_m3v3(ori, origin) + rd_f3(cam, 48);
+}
+
+// The bounce-loop head (path_tracer.hh:699-702): tangent-space view vector.
+PTG_D f3 tangent_view(f3 ray_dir, const HitInfo& info)
+{
+    f3 view = mul_v3m3(-ray_dir, info.tbn);
+    if(view.z < 1e-7f) view.z = gmax(view.z, 1e-7f);
+    return normalize(view);
+}
+
+// After tracing bounce ray `ray_dir` from `ray_o` (path_tracer.hh:722-737):
+// MIS, throughput, atmosphere, contribution, path-space regularisation.
+PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& info, f3 batt, float bpdf,
+                       f3& attenuation, f3& contribution, float& regularization)
+{
+    const float mis_pdf = bpdf < 0 ? -bpdf : (info.nee_pdf * info.nee_pdf + bpdf * bpdf) / bpdf;
+    attenuation = attenuation * batt;
+    f3 aatt, insc;
+    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc);
+    const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
+    contribution = contribution + term / mis_pdf;
+    attenuation = attenuation * (aatt / fabsf(bpdf));
+    if(bpdf > 0.0f)
+        regularization = (float)((double)regularization *
+                                 gmax_d(1.0 - (double)REGULARIZATION_GAMMA / dpow((double)bpdf, 0.25), 0.0));
+    info.roughness = 1.0f - (1.0f - info.roughness) * regularization;
+}
+
+// path_trace_pixel (path_tracer.hh:637-741) as one device function (used by
+// the per-sample entry point; the frame renderer runs the same steps as a
+// wavefront pipeline, csrc/device/wavefront.h).
+template<bool COUNT>
+PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
+{
+    const uint8_t* sf = subframe_of(sc, sample_index);
+    const uint32_t tc = rd_u(sf, SF_TLAS), to = rd_u(sf, SF_TLAS + 4);
+    const Light L = light_of(sf);
+    u4 seed;
+    f3 ray_o, ray_dir;
+    camera_ray(sc, sf, px, py, sample_index, seed, ray_o, ray_dir);
 
     HitInfo info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, 0.0f, cnt);
     f3 attenuation, in_scatter;
@@ -630,13 +742,9 @@ PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t
     float regularization = 1.0f;
     for(uint32_t bounce = 0; bounce < sc.max_bounces && info.thit > 0; ++bounce)
     {
-        Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
-        f3 view = mul_v3m3(-ray_dir, info.tbn);
-        if(view.z < 1e-7f) view.z = gmax(view.z, 1e-7f);
-        view = normalize(view);
-
+        const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
+        const f3 view = tangent_view(ray_dir, info);
         contribution = contribution + attenuation * nee_branch<COUNT>(sc, tc, to, seed, L, info, M, view, cnt);
-
         const f4 ub = uniform4(seed);
         f3 tdir, batt;
         float bpdf;
@@ -644,18 +752,7 @@ PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t
         ray_dir = normalize(mul_m3v3(info.tbn, tdir));
         ray_o = info.pos;
         info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, MIN_RAY_DIST, cnt);
-
-        const float mis_pdf = bpdf < 0 ? -bpdf : (info.nee_pdf * info.nee_pdf + bpdf * bpdf) / bpdf;
-        attenuation = attenuation * batt;
-        f3 aatt, insc;
-        atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc);
-        const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
-        contribution = contribution + term / mis_pdf;
-        attenuation = attenuation * (aatt / fabsf(bpdf));
-        if(bpdf > 0.0f)
-            regularization = (float)((double)regularization *
-                                     gmax_d(1.0 - (double)REGULARIZATION_GAMMA / dpow((double)bpdf, 0.25), 0.0));
-        info.roughness = 1.0f - (1.0f - info.roughness) * regularization;
+        bounce_tail(seed, L, ray_o, ray_dir, info, batt, bpdf, attenuation, contribution, regularization);
     }
     return contribution;
 }

@@ -1,0 +1,162 @@
+// Wavefront execution of path_trace_pixel (path_tracer.hh:637-741).
+//
+// The megakernel form (path_trace_sample) keeps a whole path in one lane, so
+// a wave lives as long as its longest path and the BVH walk runs at the
+// occupancy the shading code's registers allow.  Here one sample's path is
+// cut at its ray queries into kernels that each run over a compacted queue of
+// live paths:
+//
+//   camera   seed, film jitter, camera ray                          (:655-671)
+//   extend   closest-hit BVH walk of every queued ray                (:686, :720)
+//   shadow   any-hit walk of every pending NEE ray                   (:606-608)
+//   shade    NEE finish of the previous bounce, MIS / throughput /
+//            atmosphere of this ray, then NEE setup + BSDF sample of
+//            the next bounce, or retire the path                     (:691-737)
+//
+// Per path the arithmetic, its order and the RNG draws are exactly those of
+// path_trace_sample (same helper functions), only the place where each step
+// runs changes - the frame result stays bit-identical to the reference.
+//
+// Path state is kept in queue order (structure of arrays, one 16-byte record
+// per field), so every kernel reads and writes it with fully coalesced
+// dwordx4 accesses; survivors are appended with one atomic per wave.
+#pragma once
+#include "path_tracer.h"
+
+namespace ptg {
+namespace dm {
+
+// One ping-pong half of the path state.  Index = queue position.
+struct PathSoA {
+    uint4* meta;      // slot (sample-buffer index), round | NEE-pending << 8 | subframe << 16, TLAS node count, TLAS node offset
+    uint4* seed;      // RNG state
+    float4* ray_o;    // ray origin (= NEE shadow-ray origin)
+    float4* ray_d;    // ray direction
+    float4* att;      // throughput xyz, w = path-space regularisation
+    float4* contrib;  // contribution xyz, w = bsdf_pdf of the bounce that made this ray
+    float4* batt;     // bsdf attenuation of that bounce
+    float4* nee_c;    // pending NEE colour xyz, w = MIS pdf
+    float4* nee_d;    // pending NEE direction xyz, w = atmosphere jitter
+};
+
+// Per-queue-position results of the trace kernels.
+struct TraceOut {
+    uint4* hit;       // thit bits, instance, primitive, back_face
+    float4* bary;     // barycentrics
+    uint32_t* shadow; // 1 = the pending NEE ray is occluded
+};
+
+PTG_D uint32_t meta_round(uint4 m) { return m.y & 0xFFu; }
+PTG_D bool meta_nee(uint4 m) { return (m.y >> 8) & 1u; }
+PTG_D uint32_t meta_sub(uint4 m) { return m.y >> 16; }
+PTG_D uint32_t meta_pack(uint32_t round, bool nee, uint32_t sub) { return round | (nee ? 0x100u : 0u) | (sub << 16); }
+
+// Append `active` lanes of the calling wave to a queue; one atomic per wave.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool active)
+{
+    const unsigned long long mask = __ballot(active);
+    if(mask == 0) return 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+struct PathRec {
+    uint4 meta, seed;
+    f3 ray_o, ray_d, att, contrib, batt;
+    float reg, bpdf;
+    NeeCandidate nee;
+};
+
+PTG_D f3 xyz(float4 v) { return V3(v.x, v.y, v.z); }
+
+PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
+{
+    S.meta[q] = p.meta;
+    S.seed[q] = p.seed;
+    S.ray_o[q] = make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, 0.f);
+    S.ray_d[q] = make_float4(p.ray_d.x, p.ray_d.y, p.ray_d.z, 0.f);
+    S.att[q] = make_float4(p.att.x, p.att.y, p.att.z, p.reg);
+    S.contrib[q] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf);
+    S.batt[q] = make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f);
+    S.nee_c[q] = make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf);
+    S.nee_d[q] = make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter);
+}
+
+PTG_D PathRec load_path(const PathSoA& S, uint32_t q)
+{
+    PathRec p;
+    p.meta = S.meta[q];
+    p.seed = S.seed[q];
+    p.ray_o = xyz(S.ray_o[q]);
+    p.ray_d = xyz(S.ray_d[q]);
+    const float4 a = S.att[q], c = S.contrib[q], nc = S.nee_c[q], nd = S.nee_d[q];
+    p.att = xyz(a);
+    p.reg = a.w;
+    p.contrib = xyz(c);
+    p.bpdf = c.w;
+    p.batt = xyz(S.batt[q]);
+    p.nee.color = xyz(nc);
+    p.nee.mis_pdf = nc.w;
+    p.nee.dir = xyz(nd);
+    p.nee.jitter = nd.w;
+    return p;
+}
+
+PTG_D u4 to_u4(uint4 v) { return u4{v.x, v.y, v.z, v.w}; }
+PTG_D uint4 to_uint4(u4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+// Shade one queued path after its current ray was traced (and its pending
+// NEE ray, if any, tested).  Returns true when the path continues; `next` is
+// then the state for the next round.
+template<bool COUNT>
+PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occluded, float4* out_samples,
+                      Counters& cnt)
+{
+    const uint8_t* sf = sc.subframes + size_t(meta_sub(p.meta)) * SF_STRIDE;
+    const Light L = light_of(sf);
+    const uint32_t round = meta_round(p.meta);
+    u4 seed = to_u4(p.seed);
+    HitInfo info = hit_info<COUNT>(sc, L, p.ray_o, p.ray_d, h, cnt);
+    if(round == 0)
+    {   // primary ray (path_tracer.hh:686-693)
+        f3 attenuation, in_scatter;
+        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter);
+        p.att = attenuation;
+        p.contrib = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
+        p.reg = 1.0f;
+    }
+    else
+    {   // end of bounce round-1: its NEE term, then the bounce ray's tail
+        f3 nee = V3(0, 0, 0);
+        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o);
+        p.contrib = p.contrib + p.att * nee;
+        bounce_tail(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg);
+    }
+    if(!(round < sc.max_bounces && info.thit > 0))
+    {
+        out_samples[p.meta.x] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f);
+        return false;
+    }
+    // bounce `round` (path_tracer.hh:699-720): NEE setup, BSDF sample, next ray
+    const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
+    const f3 view = tangent_view(p.ray_d, info);
+    const bool pending = nee_prepare(seed, L, info, M, view, p.nee);
+    const f4 ub = uniform4(seed);
+    f3 tdir, batt;
+    float bpdf;
+    bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf);
+    p.ray_d = normalize(mul_m3v3(info.tbn, tdir));
+    p.ray_o = info.pos;
+    p.batt = batt;
+    p.bpdf = bpdf;
+    p.seed = to_uint4(seed);
+    p.meta.y = meta_pack(round + 1, pending, meta_sub(p.meta));
+    return true;
+}
+
+} // namespace dm
+} // namespace ptg

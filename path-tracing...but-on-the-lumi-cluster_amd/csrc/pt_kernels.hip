@@ -17,6 +17,7 @@
 #include "ptg.h"
 #include "device/layout.h"
 #include "device/path_tracer.h"
+#include "device/wavefront.h"
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -109,18 +110,168 @@ struct PixelMap {
     }
 };
 
-struct CounterSink {
-    unsigned long long* dev;   // [8]
-};
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
+{
+    unsigned long long s = v;
+    for(int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    return s;
+}
 
+// Counting builds only: wave-reduce the counters, one atomic per counter per wave.
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* dev, uint32_t samples)
 {
-    atomicAdd(dev + 0, (unsigned long long)samples);
-    atomicAdd(dev + 1, (unsigned long long)c.visits);
-    atomicAdd(dev + 2, (unsigned long long)c.tri_tests);
-    atomicAdd(dev + 3, (unsigned long long)c.blas_entries);
-    atomicAdd(dev + 4, (unsigned long long)c.queries);
-    atomicAdd(dev + 5, (unsigned long long)c.shades);
+    const unsigned long long v[6] = {wave_sum(samples), wave_sum(c.visits), wave_sum(c.tri_tests),
+                                     wave_sum(c.blas_entries), wave_sum(c.queries), wave_sum(c.shades)};
+    if((threadIdx.x & 63u) == 0)
+        for(int k = 0; k < 6; ++k)
+            if(v[k]) atomicAdd(dev + k, v[k]);
+}
+
+// ---- wavefront pipeline (csrc/device/wavefront.h) ----
+
+// Lane -> (pixel, sample) of a chunk: a wave holds 8 pixels x 8 consecutive
+// samples (one motion-blur subframe); consecutive waves walk the sample
+// groups of one pixel group.
+__device__ __forceinline__ void chunk_coords(uint32_t i, uint32_t nj, uint32_t& p, uint32_t& jj)
+{
+    const uint32_t wave = i >> 6, lane = i & 63u;
+    const uint32_t sgroups = (nj + 7u) >> 3;
+    jj = (wave % sgroups) * 8u + (lane & 7u);
+    p = (wave / sgroups) * 8u + (lane >> 3);
+}
+
+// counts[2r]: paths queued for round r; counts[2r+1]: their pending NEE rays.
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, uint32_t j0, uint32_t nj, uint32_t M,
+                                                      PathSoA S, uint32_t* __restrict__ counts, float4* __restrict__ out,
+                                                      unsigned long long* __restrict__ counters)
+{
+    uint32_t lives = 0;
+    for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x)
+    {
+        uint32_t p, jj, x = 0, y = 0;
+        chunk_coords(i, nj, p, jj);
+        const bool in_chunk = p < pm.npix && jj < nj;
+        const bool live = in_chunk && pm.pixel(p, x, y);
+        const uint32_t slot = jj * pm.npix + p;
+        if(in_chunk && !live) out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint32_t q = wave_append(&counts[0], live);
+        if(live)
+        {
+            const int32_t j = (int32_t)(j0 + jj);
+            const uint8_t* sf = subframe_of(sc, j);
+            PathRec r;
+            u4 seed;
+            camera_ray(sc, sf, x, y, j, seed, r.ray_o, r.ray_d);
+            r.meta = make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE), rd_u(sf, SF_TLAS),
+                                rd_u(sf, SF_TLAS + 4));
+            r.seed = to_uint4(seed);
+            r.att = r.contrib = r.batt = V3(0, 0, 0);
+            r.reg = 1.0f;
+            r.bpdf = 0.0f;
+            r.nee = NeeCandidate{V3(0, 0, 0), V3(0, 0, 0), 0.0f, 0.0f};
+            store_path(S, q, r);
+            ++lives;
+        }
+    }
+    if(COUNT) flush_counters(Counters{}, counters, lives);
+}
+
+// BVH walks of one round over a queue: ANY = false walks the extension rays
+// (closest hit, queue positions 0..n-1), ANY = true the pending NEE rays
+// (any hit, positions from the NEE list).  Persistent "while-while" loop:
+// the grid is sized to what is resident, each wave owns a contiguous range of
+// the queue (no atomics), and a lane that finishes its ray takes the next one
+// of its wave's range, so the wave never idles behind its longest ray.
+constexpr int kRefillIdle = 16;   // refill once at least this many lanes are idle
+
+template<bool ANY, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, const uint32_t* __restrict__ counts,
+                                                    uint32_t round, const uint32_t* __restrict__ list, TraceOut tr,
+                                                    unsigned long long* __restrict__ counters)
+{
+    const uint32_t n = counts[2 * round + (ANY ? 1 : 0)];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    uint32_t cursor = uint32_t((uint64_t(n) * wave) / waves);
+    const uint32_t end = uint32_t((uint64_t(n) * (wave + 1)) / waves);
+    const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
+    const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
+    Counters cnt;
+    Walker w;
+    bool active = false;
+    uint32_t q = 0;
+    for(;;)
+    {
+        if(cursor < end)
+        {
+            const unsigned long long idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if(nidle >= (uint32_t)kRefillIdle || nidle == 64u)
+            {
+                if(!active)
+                {
+                    const uint32_t t = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                    if(t < end)
+                    {
+                        q = ANY ? list[t] : t;
+                        const uint4 m = S.meta[q];
+                        w.init(sc, m.z, m.w, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
+                        active = true;
+                        if(COUNT) cnt.queries++;
+                    }
+                }
+                cursor = min(end, cursor + nidle);
+            }
+        }
+        if(!__any(active)) break;
+        if(active)
+        {
+            const int r = w.template step<ANY, COUNT>(sc, cnt);
+            if(r != 0)
+            {
+                if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
+                else
+                {
+                    const Hit& h = w.best;
+                    tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
+                    tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
+                }
+                active = false;
+            }
+        }
+    }
+    if(COUNT) flush_counters(cnt, counters, 0);
+}
+
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
+                                                     uint32_t round, TraceOut tr, uint32_t* __restrict__ next_list,
+                                                     float4* __restrict__ out, unsigned long long* __restrict__ counters)
+{
+    const uint32_t n = counts[2 * round];
+    Counters cnt;
+    for(uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x)
+    {
+        PathRec p = load_path(cur, q);
+        const uint4 hv = tr.hit[q];
+        const float4 bv = tr.bary[q];
+        Hit h;
+        h.thit = __uint_as_float(hv.x);
+        h.instance_id = hv.y;
+        h.primitive_id = hv.z;
+        h.back_face = hv.w != 0;
+        h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
+        const bool occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
+        const bool cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
+        const bool nee = cont && meta_nee(p.meta);
+        const uint32_t qn = wave_append(&counts[2 * (round + 1)], cont);
+        const uint32_t sn = wave_append(&counts[2 * (round + 1) + 1], nee);
+        if(cont) store_path(nxt, qn, p);
+        if(nee) next_list[sn] = qn;
+    }
+    if(COUNT) flush_counters(cnt, counters, 0);
 }
 
 // One work-item per (pixel, sample).  A wave holds 8 pixels x 8 consecutive
@@ -148,8 +299,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene sc, PixelMap pm, uint
             r = make_float4(c.x, c.y, c.z, 0.f);
         }
         out[size_t(jj) * pm.npix + p] = r;
-        if(COUNT) flush_counters(cnt, counters, 1);
     }
+    if(COUNT) flush_counters(cnt, counters, (p < pm.npix && jj < nj) ? 1u : 0u);
 }
 
 // acc[p] (+)= samples in index order; on the last chunk / spp and tonemap.
@@ -293,7 +444,14 @@ struct ptg_context {
     // k_trace launch timing (HIP events on the launch stream)
     bool timing = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
+    std::vector<int> ev_kind;
     size_t ev_used = 0;
+    // 0: wavefront pipeline (default), 1: megakernel
+    int pipeline = 0;
+    uint32_t persistent_blocks = 2048;
+    uint32_t walk_grid[2] = {2048, 2048};   // resident blocks of k_wf_walk<closest/any>
+    DevBuf wf_state;
+    uint64_t kind_counters[6][8] = {};
     ~ptg_context()
     {
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
@@ -350,64 +508,186 @@ int check_cfg(const ptg_context* ctx, const ptg_render_config* cfg, uint32_t sam
     return PTG_OK;
 }
 
-// Render the pixels of `pm` for samples [j0, j1): chunked trace + ordered accumulate.
+// Kernel kinds for timing and work counters.
+enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA = 4, K_ACCUM = 5, K_KINDS = 6 };
+
+int timed_begin(ptg_context* ctx, int kind);
+int timed_end(ptg_context* ctx);
+
+// Render the pixels of `pm` for samples [j0, j1): per chunk of samples, the
+// path kernels write one float4 per (pixel, sample); k_accumulate folds the
+// chunk into the running per-pixel sum in sample order.
 int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint32_t j0, uint32_t j1,
                ptg_float4* out_accum, ptg_uchar4* out_bgra)
 {
     if(pm.npix == 0) return PTG_OK;
     if(j1 <= j0) return fail(PTG_E_INVALID, "empty sample range");
-    const size_t budget = size_t(1) << 30;                       // per-sample buffer <= 1 GiB
-    uint32_t chunk = uint32_t(std::max<size_t>(8, budget / (size_t(pm.npix) * sizeof(float4))));
+    const bool wf = ctx->pipeline == 0;
+    // samples per chunk: megakernel <= 1 GiB of results; wavefront ~16 M live paths
+    const size_t target = wf ? (size_t(1) << 24) : ((size_t(1) << 30) / sizeof(float4));
+    uint32_t chunk = uint32_t(std::max<size_t>(8, target / size_t(pm.npix)));
     chunk = std::min<uint32_t>(chunk & ~7u, j1 - j0);
     if(chunk == 0) chunk = std::min<uint32_t>(8, j1 - j0);
+    const size_t M = size_t((pm.npix + 7) / 8) * ((chunk + 7) / 8) * 64;   // lanes per chunk (upper bound)
+    if(M >= (1ull << 31)) return fail(PTG_E_RANGE, "chunk too large");
     PTG_HIP(ctx->samples.reserve(size_t(pm.npix) * chunk * sizeof(float4)));
     PTG_HIP(ctx->acc.reserve(size_t(pm.npix) * sizeof(float4)));
+    unsigned long long* cnt_dev = nullptr;
     if(ctx->counting)
     {
-        PTG_HIP(ctx->counters.reserve(8 * sizeof(unsigned long long)));
-        PTG_HIP(hipMemsetAsync(ctx->counters.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+        PTG_HIP(ctx->counters.reserve(K_KINDS * 8 * sizeof(unsigned long long)));
+        PTG_HIP(hipMemsetAsync(ctx->counters.p, 0, K_KINDS * 8 * sizeof(unsigned long long), ctx->stream));
+        cnt_dev = ctx->counters.as<unsigned long long>();
+    }
+    const uint32_t rounds = cfg->max_bounces + 1;
+    PathSoA S[2];
+    TraceOut tr{};
+    uint32_t* lists[2] = {nullptr, nullptr};
+    uint32_t* counts = nullptr;
+    uint32_t* heads = nullptr;
+    if(wf)
+    {
+        // path state: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
+        const size_t rec = M * 16;
+        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + M * (16 + 16 + 4) + 2 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+        char* b = ctx->wf_state.as<char>();
+        for(int h = 0; h < 2; ++h)
+        {
+            S[h].meta = reinterpret_cast<uint4*>(b); b += rec;
+            S[h].seed = reinterpret_cast<uint4*>(b); b += rec;
+            S[h].ray_o = reinterpret_cast<float4*>(b); b += rec;
+            S[h].ray_d = reinterpret_cast<float4*>(b); b += rec;
+            S[h].att = reinterpret_cast<float4*>(b); b += rec;
+            S[h].contrib = reinterpret_cast<float4*>(b); b += rec;
+            S[h].batt = reinterpret_cast<float4*>(b); b += rec;
+            S[h].nee_c = reinterpret_cast<float4*>(b); b += rec;
+            S[h].nee_d = reinterpret_cast<float4*>(b); b += rec;
+        }
+        tr.hit = reinterpret_cast<uint4*>(b); b += M * 16;
+        tr.bary = reinterpret_cast<float4*>(b); b += M * 16;
+        tr.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        counts = reinterpret_cast<uint32_t*>(b);
+        heads = counts + 2 * (rounds + 2);
     }
     const DevScene sc = ctx->scene_args(cfg);
+    const uint32_t persistent = ctx->persistent_blocks;
+    auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
     ctx->ev_used = 0;
     for(uint32_t j = j0; j < j1; j += chunk)
     {
         const uint32_t nj = std::min(chunk, j1 - j);
-        const size_t waves = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8);
-        const size_t threads = waves * 64;
-        if(threads / kBlock + 1 > 0x7FFFFFFFull) return fail(PTG_E_RANGE, "launch too large");
-        if(ctx->timing)
+        const size_t lanes = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8) * 64;
+        float4* out = ctx->samples.as<float4>();
+        if(!wf)
         {
-            if(ctx->ev_used == ctx->ev_start.size())
-            {
-                hipEvent_t a, b;
-                PTG_HIP(hipEventCreate(&a));
-                PTG_HIP(hipEventCreate(&b));
-                ctx->ev_start.push_back(a);
-                ctx->ev_stop.push_back(b);
-            }
-            PTG_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+            if(int r = timed_begin(ctx, K_MEGA)) return r;
+            if(ctx->counting)
+                hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(lanes)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, out,
+                                   cnt_for(K_MEGA));
+            else
+                hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(lanes)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, out,
+                                   nullptr);
+            PTG_HIP(hipGetLastError());
+            if(int r = timed_end(ctx)) return r;
         }
-        if(ctx->counting)
-            hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(threads)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj,
-                               ctx->samples.as<float4>(), ctx->counters.as<unsigned long long>());
         else
-            hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(threads)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj,
-                               ctx->samples.as<float4>(), nullptr);
-        PTG_HIP(hipGetLastError());
-        if(ctx->timing) PTG_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used++], ctx->stream));
+        {
+            PTG_HIP(hipMemsetAsync(counts, 0, 4 * (rounds + 2) * sizeof(uint32_t), ctx->stream));
+            const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(persistent, grid_for(lanes))));
+            if(int r = timed_begin(ctx, K_CAMERA)) return r;
+            if(ctx->counting)
+                hipLaunchKernelGGL(k_wf_camera<true>, grid, dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, uint32_t(lanes),
+                                   S[0], counts, out, cnt_for(K_CAMERA));
+            else
+                hipLaunchKernelGGL(k_wf_camera<false>, grid, dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, uint32_t(lanes),
+                                   S[0], counts, out, nullptr);
+            PTG_HIP(hipGetLastError());
+            if(int r = timed_end(ctx)) return r;
+            for(uint32_t r = 0; r < rounds; ++r)
+            {
+                const PathSoA& cur = S[r & 1];
+                const PathSoA& nxt = S[(r + 1) & 1];
+                if(int e = timed_begin(ctx, K_EXTEND)) return e;
+                if(ctx->counting)
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
+                                       counts, r, nullptr, tr, cnt_for(K_EXTEND));
+                else
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
+                                       counts, r, nullptr, tr, nullptr);
+                PTG_HIP(hipGetLastError());
+                if(int e = timed_end(ctx)) return e;
+                if(r > 0)
+                {
+                    if(int e = timed_begin(ctx, K_SHADOW)) return e;
+                    if(ctx->counting)
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
+                                           cur, counts, r, lists[r & 1], tr, cnt_for(K_SHADOW));
+                    else
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
+                                           cur, counts, r, lists[r & 1], tr, nullptr);
+                    PTG_HIP(hipGetLastError());
+                    if(int e = timed_end(ctx)) return e;
+                }
+                if(int e = timed_begin(ctx, K_SHADE)) return e;
+                if(ctx->counting)
+                    hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
+                                       lists[(r + 1) & 1], out, cnt_for(K_SHADE));
+                else
+                    hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
+                                       lists[(r + 1) & 1], out, nullptr);
+                PTG_HIP(hipGetLastError());
+                if(int e = timed_end(ctx)) return e;
+            }
+        }
         const int first = j == j0, last = j + nj >= j1;
+        if(int r = timed_begin(ctx, K_ACCUM)) return r;
         hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, ctx->stream, pm, nj,
                            ctx->samples.as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
                            reinterpret_cast<float4*>(out_accum), reinterpret_cast<uchar4*>(out_bgra));
         PTG_HIP(hipGetLastError());
+        if(int r = timed_end(ctx)) return r;
     }
     if(ctx->counting)
     {
-        unsigned long long host[8];
+        unsigned long long host[K_KINDS * 8];
         PTG_HIP(hipMemcpyAsync(host, ctx->counters.p, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
         PTG_HIP(hipStreamSynchronize(ctx->stream));
-        for(int i = 0; i < 8; ++i) ctx->last_counters[i] = host[i];
+        for(int i = 0; i < 8; ++i)
+        {
+            ctx->last_counters[i] = 0;
+            for(int k = 0; k < K_KINDS; ++k)
+            {
+                ctx->kind_counters[k][i] = host[k * 8 + i];
+                ctx->last_counters[i] += host[k * 8 + i];
+            }
+        }
     }
+    return PTG_OK;
+}
+
+int timed_begin(ptg_context* ctx, int kind)
+{
+    if(!ctx->timing) return PTG_OK;
+    if(ctx->ev_used == ctx->ev_start.size())
+    {
+        hipEvent_t a, b;
+        PTG_HIP(hipEventCreate(&a));
+        PTG_HIP(hipEventCreate(&b));
+        ctx->ev_start.push_back(a);
+        ctx->ev_stop.push_back(b);
+        ctx->ev_kind.push_back(0);
+    }
+    ctx->ev_kind[ctx->ev_used] = kind;
+    PTG_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+    return PTG_OK;
+}
+
+int timed_end(ptg_context* ctx)
+{
+    if(!ctx->timing) return PTG_OK;
+    PTG_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used++], ctx->stream));
     return PTG_OK;
 }
 
@@ -446,6 +726,16 @@ int ptg_context_create(int device, ptg_context** out)
     ctx->device = device;
     const char* cnt = getenv("PTG_COUNTERS");
     ctx->counting = cnt && cnt[0] == '1';
+    const char* pipe = getenv("PTG_PIPELINE");
+    if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
+    ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 8;
+    // the walk kernels split their queue statically over the waves of the grid,
+    // so the grid must be exactly what is resident at once
+    int per_cu = 0;
+    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, 0) == hipSuccess && per_cu > 0)
+        ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
+    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, 0) == hipSuccess && per_cu > 0)
+        ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
     PTG_HIP(hipSetDevice(device));
     *out = ctx.release();
     return PTG_OK;
@@ -764,20 +1054,46 @@ int ptg_timing_enable(ptg_context* ctx, int enable)
     return PTG_OK;
 }
 
-int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches)
+int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8])
 {
     if(int r = bind(ctx)) return r;
-    if(!trace_ms || !launches) return fail(PTG_E_INVALID, "ptg_last_timing: bad arguments");
-    double total = 0;
+    if(!ms || !launches) return fail(PTG_E_INVALID, "ptg_last_kernel_times: bad arguments");
+    for(int k = 0; k < 8; ++k) { ms[k] = 0; launches[k] = 0; }
     for(size_t i = 0; i < ctx->ev_used; ++i)
     {
         PTG_HIP(hipEventSynchronize(ctx->ev_stop[i]));
-        float ms = 0;
-        PTG_HIP(hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
-        total += ms;
+        float t = 0;
+        PTG_HIP(hipEventElapsedTime(&t, ctx->ev_start[i], ctx->ev_stop[i]));
+        ms[ctx->ev_kind[i]] += t;
+        launches[ctx->ev_kind[i]] += 1;
     }
-    *trace_ms = total;
-    *launches = uint32_t(ctx->ev_used);
+    return PTG_OK;
+}
+
+int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches)
+{
+    if(!trace_ms || !launches) return fail(PTG_E_INVALID, "ptg_last_timing: bad arguments");
+    double ms[8];
+    uint32_t n[8];
+    if(int r = ptg_last_kernel_times(ctx, ms, n)) return r;
+    *trace_ms = 0;
+    *launches = 0;
+    for(int k = 0; k < K_ACCUM; ++k) { *trace_ms += ms[k]; *launches += n[k]; }
+    return PTG_OK;
+}
+
+int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8])
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_kernel_counters: bad arguments");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable or PTG_COUNTERS=1)");
+    memcpy(out, ctx->kind_counters, sizeof(ctx->kind_counters));
+    return PTG_OK;
+}
+
+int ptg_set_pipeline(ptg_context* ctx, int pipeline)
+{
+    if(!ctx || pipeline < 0 || pipeline > 1) return fail(PTG_E_INVALID, "ptg_set_pipeline: 0 = wavefront, 1 = megakernel");
+    ctx->pipeline = pipeline;
     return PTG_OK;
 }
 

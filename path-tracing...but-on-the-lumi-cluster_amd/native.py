@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libptg.so")
+LIB_PATH = os.environ.get("PTG_LIB") or os.path.join(HERE, "_build", "libptg.so")
 
 PTG_OK = 0
 
@@ -107,6 +107,9 @@ def lib():
         "ptg_last_counters": (I, [P, P]),
         "ptg_timing_enable": (I, [P, I]),
         "ptg_last_timing": (I, [P, C.POINTER(C.c_double), C.POINTER(U32)]),
+        "ptg_last_kernel_times": (I, [P, P, P]),
+        "ptg_last_kernel_counters": (I, [P, P]),
+        "ptg_set_pipeline": (I, [P, I]),
         "ptg_synchronize": (I, [P]),
         "ptg_device_alloc": (I, [P, SZ, C.POINTER(P)]),
         "ptg_device_free": (I, [P, P]),

@@ -143,6 +143,25 @@ class GpuRenderer:
         N.check(N.lib().ptg_last_timing(self._ctx, C.byref(ms), C.byref(n)), "ptg_last_timing")
         return ms.value, n.value
 
+    KINDS = ("megakernel", "extend", "shadow", "shade", "camera", "accumulate")
+
+    def kernel_times(self):
+        """{kind: (device ms, launches)} of the last render call (timing enabled)."""
+        ms = np.zeros(8, np.float64)
+        n = np.zeros(8, np.uint32)
+        N.check(N.lib().ptg_last_kernel_times(self._ctx, ms.ctypes.data, n.ctypes.data), "ptg_last_kernel_times")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KINDS)}
+
+    def kernel_counters(self):
+        """{kind: counters[8]} of the last render call (counting enabled)."""
+        out = np.zeros((6, 8), np.uint64)
+        N.check(N.lib().ptg_last_kernel_counters(self._ctx, out.ctypes.data), "ptg_last_kernel_counters")
+        return {k: out[i] for i, k in enumerate(self.KINDS)}
+
+    def set_pipeline(self, name):
+        """'wavefront' (default) or 'megakernel' - bit-identical results."""
+        N.check(N.lib().ptg_set_pipeline(self._ctx, {"wavefront": 0, "megakernel": 1}[name]), "ptg_set_pipeline")
+
     def enable_counters(self, on=True):
         N.check(N.lib().ptg_counters_enable(self._ctx, 1 if on else 0), "ptg_counters_enable")
 

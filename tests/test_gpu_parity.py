@@ -92,3 +92,19 @@ def test_rays_bit_exact(gpu, assets_dir):
     want = Oracle(arr, s.cfg).trace_rays(1, rays)
     assert (want[:, 3].view(np.float32) > 0).sum() > n // 10      # the set actually hits geometry
     assert np.array_equal(got, want)
+
+
+def test_pipelines_identical(gpu, assets_dir):
+    """Wavefront and megakernel executions give the same bits (frame 450, 64x36 crop, 24 spp)."""
+    W, H, SPP = 640, 360, 32
+    s = scene_for(assets_dir, W, H, SPP, frame=450)
+    gpu.upload_arrays(arrays_copy(s))
+    outs = []
+    for p in ("wavefront", "megakernel"):
+        gpu.set_pipeline(p)
+        bgra, acc = gpu.render(s.cfg, rect=(300, 150, 64, 36), samples=(0, 24), want_accum=True)
+        gpu.synchronize()
+        outs.append((bgra.cpu().numpy(), acc.cpu().numpy()))
+    gpu.set_pipeline("wavefront")
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(_bits(outs[0][1]), _bits(outs[1][1]))
