@@ -46,6 +46,7 @@ struct TraceOut {
     uint32_t* shadow; // 1 = the pending NEE ray is occluded
 };
 
+constexpr uint32_t META_DEAD = 0x200u;   // queue entry with no path (outside the chunk / image)
 PTG_D uint32_t meta_round(uint4 m) { return m.y & 0xFFu; }
 PTG_D bool meta_nee(uint4 m) { return (m.y >> 8) & 1u; }
 PTG_D uint32_t meta_sub(uint4 m) { return m.y >> 16; }
@@ -116,6 +117,7 @@ template<bool COUNT>
 PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occluded, float4* out_samples,
                       Counters& cnt)
 {
+    if(p.meta.y & META_DEAD) return false;
     const uint8_t* sf = sc.subframes + size_t(meta_sub(p.meta)) * SF_STRIDE;
     const Light L = light_of(sf);
     const uint32_t round = meta_round(p.meta);

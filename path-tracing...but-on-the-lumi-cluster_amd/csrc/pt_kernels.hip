@@ -141,11 +141,15 @@ __device__ __forceinline__ void chunk_coords(uint32_t i, uint32_t nj, uint32_t& 
 }
 
 // counts[2r]: paths queued for round r; counts[2r+1]: their pending NEE rays.
+// Round 0 is every lane of the chunk in lane order (queue position = lane, no
+// compaction); lanes outside the chunk or the image are queued as dead paths
+// (an empty TLAS, retired by the first shade).
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, uint32_t j0, uint32_t nj, uint32_t M,
                                                       PathSoA S, uint32_t* __restrict__ counts, float4* __restrict__ out,
                                                       unsigned long long* __restrict__ counters)
 {
+    if(blockIdx.x == 0 && threadIdx.x == 0) counts[0] = M;
     uint32_t lives = 0;
     for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x)
     {
@@ -153,26 +157,26 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
         chunk_coords(i, nj, p, jj);
         const bool in_chunk = p < pm.npix && jj < nj;
         const bool live = in_chunk && pm.pixel(p, x, y);
-        const uint32_t slot = jj * pm.npix + p;
-        if(in_chunk && !live) out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const uint32_t q = wave_append(&counts[0], live);
-        if(live)
+        const uint32_t slot = in_chunk ? jj * pm.npix + p : 0xFFFFFFFFu;
+        if(!live)
         {
-            const int32_t j = (int32_t)(j0 + jj);
-            const uint8_t* sf = subframe_of(sc, j);
-            PathRec r;
-            u4 seed;
-            camera_ray(sc, sf, x, y, j, seed, r.ray_o, r.ray_d);
-            r.meta = make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE), rd_u(sf, SF_TLAS),
-                                rd_u(sf, SF_TLAS + 4));
-            r.seed = to_uint4(seed);
-            r.att = r.contrib = r.batt = V3(0, 0, 0);
-            r.reg = 1.0f;
-            r.bpdf = 0.0f;
-            r.nee = NeeCandidate{V3(0, 0, 0), V3(0, 0, 0), 0.0f, 0.0f};
-            store_path(S, q, r);
-            ++lives;
+            if(in_chunk) out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+            S.meta[i] = make_uint4(slot, META_DEAD, 0u, 0u);
+            S.ray_o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            S.ray_d[i] = make_float4(0.f, 0.f, 1.f, 0.f);
+            continue;
         }
+        const int32_t j = (int32_t)(j0 + jj);
+        const uint8_t* sf = subframe_of(sc, j);
+        u4 seed;
+        f3 o, d;
+        camera_ray(sc, sf, x, y, j, seed, o, d);
+        S.meta[i] = make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE), rd_u(sf, SF_TLAS),
+                               rd_u(sf, SF_TLAS + 4));
+        S.seed[i] = to_uint4(seed);
+        S.ray_o[i] = make_float4(o.x, o.y, o.z, 0.f);
+        S.ray_d[i] = make_float4(d.x, d.y, d.z, 0.f);
+        ++lives;
     }
     if(COUNT) flush_counters(Counters{}, counters, lives);
 }
@@ -192,10 +196,14 @@ __global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, cons
 {
     const uint32_t n = counts[2 * round + (ANY ? 1 : 0)];
     const uint32_t lane = threadIdx.x & 63u;
+    // wave w takes the 64-entry groups w, w + W, w + 2W, ... of the queue: every
+    // wave samples the whole image (balanced), each group is 8 pixels x 8
+    // samples (coherent)
     const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    uint32_t cursor = uint32_t((uint64_t(n) * wave) / waves);
-    const uint32_t end = uint32_t((uint64_t(n) * (wave + 1)) / waves);
+    const uint32_t groups = (n + 63u) >> 6;
+    const uint32_t end = wave < groups ? ((groups - wave + waves - 1) / waves) * 64u : 0u;
+    uint32_t cursor = 0;
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
@@ -212,8 +220,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, cons
             {
                 if(!active)
                 {
-                    const uint32_t t = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                    if(t < end)
+                    const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                    const uint32_t t = (wave + (v >> 6) * waves) * 64u + (v & 63u);
+                    if(v < end && t < n)
                     {
                         q = ANY ? list[t] : t;
                         const uint4 m = S.meta[q];
@@ -544,7 +553,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     TraceOut tr{};
     uint32_t* lists[2] = {nullptr, nullptr};
     uint32_t* counts = nullptr;
-    uint32_t* heads = nullptr;
     if(wf)
     {
         // path state: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
@@ -569,7 +577,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
         lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
         counts = reinterpret_cast<uint32_t*>(b);
-        heads = counts + 2 * (rounds + 2);
     }
     const DevScene sc = ctx->scene_args(cfg);
     const uint32_t persistent = ctx->persistent_blocks;
