@@ -18,8 +18,9 @@ interleaved 32x16 tiles, rank 0 gathers the BGRA tiles over RCCL and
 assembles the framebuffer - strong scaling (config 3 style).
 
 Prints ONE JSON line (rank 0) with the driver contract fields plus
-"roofline" (k_trace: algorithmic bytes / device time from HIP events, vs
-8 TB/s HBM) and "cpu_baseline" (the reference's own baseline_render built
+"roofline" (the dominant kernel k_wf_walk<closest>: its algorithmic bytes
+from the deterministic work counters / its device time from HIP events on the
+launch stream, vs 8 TB/s HBM) and "cpu_baseline" (the reference's own baseline_render built
 from its sources, timed on this host's cores on a bounded sample).
 """
 import argparse
@@ -44,6 +45,14 @@ def algorithmic_bytes(c):
     9 x 16 B vertex attributes), 160 B subframe per sample."""
     samples, visits, tris, enters, queries, shades = [int(x) for x in c[:6]]
     return 32 * visits + 60 * tris + 88 * enters + 156 * shades + 160 * samples
+
+
+def extend_bytes(c):
+    """Algorithmic bytes of the closest-hit walk kernel: per node visit one 32 B
+    TravRec, per triangle test 60 B (3 x u32 + 3 x 16 B in reference layout),
+    per BLAS entry 88 B, plus per ray 48 B of ray state in and 32 B of hit out."""
+    visits, tris, enters, queries = int(c[1]), int(c[2]), int(c[3]), int(c[4])
+    return 32 * visits + 60 * tris + 88 * enters + 80 * queries
 
 
 def cpu_baseline(assets, frame):
@@ -126,13 +135,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(local)
     r.enable_timing(True)
-    trace_ms, trace_launches = 0.0, 0
+    step_kernel_ms, step_kernel_n = {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        ms, n = r.last_timing()       # waits for this step's k_trace launches
-        trace_ms += ms
-        trace_launches += n
+        for k, (ms, n) in r.kernel_times().items():    # waits for this step's launches
+            step_kernel_ms[k] = step_kernel_ms.get(k, 0.0) + ms
+            step_kernel_n[k] = step_kernel_n.get(k, 0) + n
     torch.cuda.synchronize(local)
     if world > 1:
         dist.barrier()
@@ -158,24 +167,32 @@ def main():
             else:
                 r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
             r.synchronize()
-            c = r.counters()
+            kc = r.kernel_counters()
             r.enable_counters(False)
-            per_step_samples = int(c[0])
-            alg = algorithmic_bytes(c)
-            launches_per_step = trace_launches / args.steps
-            ms_per_launch = trace_ms / trace_launches
-            bytes_per_launch = alg / launches_per_step
+            total = sum(kc[k] for k in kc)
+            per_step_samples = int(total[0])
+            # dominant kernel: the closest-hit BVH walk (k_wf_walk<closest>, "extend")
+            ext_ms, ext_n = step_kernel_ms["extend"], step_kernel_n["extend"]
+            ext_bytes = extend_bytes(kc["extend"])
+            ms_per_launch = ext_ms / ext_n
+            bytes_per_launch = ext_bytes / (ext_n / args.steps)
             achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9
+            path_ms = sum(step_kernel_ms[k] for k in step_kernel_ms if k != "accumulate") / args.steps
+            path_bytes = algorithmic_bytes(total)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": "k_trace", "ms_per_launch": round(ms_per_launch, 3),
-                    "launches_per_step": launches_per_step,
-                    "algorithmic_bytes_per_sample": round(alg / per_step_samples, 1),
-                    "per_sample": {"node_visits": round(c[1] / per_step_samples, 2),
-                                   "triangle_tests": round(c[2] / per_step_samples, 2),
-                                   "blas_entries": round(c[3] / per_step_samples, 2),
-                                   "ray_queries": round(c[4] / per_step_samples, 3),
-                                   "shades": round(c[5] / per_step_samples, 3)}}
+                    "kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)",
+                    "ms_per_launch": round(ms_per_launch, 4), "launches_per_step": ext_n / args.steps,
+                    "bytes_per_launch": int(bytes_per_launch),
+                    "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_kernel_ms.items()},
+                    "hot_path": {"achieved_GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
+                                 "algorithmic_bytes_per_sample": round(path_bytes / per_step_samples, 1),
+                                 "formula": "32 visits + 60 tri + 88 enter + 156 shade + 160 per sample (SURVEY 8d)"},
+                    "per_sample": {"node_visits": round(total[1] / per_step_samples, 2),
+                                   "triangle_tests": round(total[2] / per_step_samples, 2),
+                                   "blas_entries": round(total[3] / per_step_samples, 2),
+                                   "ray_queries": round(total[4] / per_step_samples, 3),
+                                   "shades": round(total[5] / per_step_samples, 3)}}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:

@@ -36,6 +36,9 @@ using namespace ptg::dm;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef PTG_SHADE_WAVES
+#define PTG_SHADE_WAVES 3
+#endif
 
 // ---------------------------------------------------------------- kernels --
 
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, cons
 }
 
 template<bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
                                                      uint32_t round, TraceOut tr, uint32_t* __restrict__ next_list,
                                                      float4* __restrict__ out, unsigned long long* __restrict__ counters)
 {
@@ -275,8 +278,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, PathSoA cur, P
         const bool occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
         const bool cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
         const bool nee = cont && meta_nee(p.meta);
+#ifdef PTG_ABLATE_NO_APPEND
+        const uint32_t qn = q, sn = q;   // timing experiment only: no compaction
+        if(q == 0) { counts[2 * (round + 1)] = n; counts[2 * (round + 1) + 1] = n; }
+#else
         const uint32_t qn = wave_append(&counts[2 * (round + 1)], cont);
         const uint32_t sn = wave_append(&counts[2 * (round + 1) + 1], nee);
+#endif
         if(cont) store_path(nxt, qn, p);
         if(nee) next_list[sn] = qn;
     }
