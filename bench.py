@@ -2,14 +2,18 @@
 """Benchmark of the hot path: path_trace_pixel -> ray_query BVH traversal ->
 tonemap_pixel under baseline_render, on MI355X.
 
-Workload (BASELINE.json configs[1]): frame 0 of the reference animation,
-1280x720, 256 samples per pixel, MAX_BOUNCES = 4 (the shipped TESTING
-preset), the reference scene (reference OBJ assets + committed substitutes for
+Workload (the configuration BASELINE.json's metric is quoted on, "1280x720
+1024spp"; configs[1] is the same frame at 256 spp): frame 0 of the reference
+animation, 1280x720, 1024 samples per pixel, MAX_BOUNCES = 4 (the shipped
+TESTING preset), the reference scene (reference OBJ assets + committed substitutes for
 the three missing meshes).  One step = what the reference does per frame
 after load_scene: setup_animation_frame (host C++) + upload of the frame's
 TLAS/instances/subframes + the full-frame render on the GPU (+ the RCCL
 framebuffer gather in --shard tiles mode), inputs of the static scene already
-resident in HBM.
+resident in HBM.  Steps are issued asynchronously, as main.cc's frame loop
+would drive the C ABI: the host setup of step k+1 runs while the GPU renders
+step k (ptg_upload_frame waits for the previous render before overwriting
+the frame buffers).
 
 Multi-GPU: one process per GPU (torch.distributed.run).  --shard frames
 (default): rank r renders frame (frame + r) - weak scaling, no collective on
@@ -34,6 +38,23 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# rocprofv3 PMC summary of this same workload (tools/profile_gpu.sh + tools/summarize_prof.py)
+TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_wavefront", "pmc_summary.json")
+
+
+def pmc_traffic(kind, workload):
+    """HBM-side bytes per launch of `kind` from the committed PMC passes
+    (FETCH_SIZE x 1 KiB x 2 per the gfx950 correction + WRITE_SIZE x 1 KiB),
+    or None when the profile is missing or was taken on another workload."""
+    try:
+        with open(TRAFFIC_PROFILE) as f:
+            prof = json.load(f)
+        if prof.get("_workload") != workload:
+            return None, None
+        d = prof[kind]["derived"]
+        return int(d["hbm_side_bytes"]), os.path.relpath(TRAFFIC_PROFILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def algorithmic_bytes(c):
@@ -79,7 +100,7 @@ def main():
     ap.add_argument("--frame", type=int, default=0)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
-    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames")
     ap.add_argument("--tile", type=str, default="32x16")
@@ -135,18 +156,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(local)
     r.enable_timing(True)
-    step_kernel_ms, step_kernel_n = {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        for k, (ms, n) in r.kernel_times().items():    # waits for this step's launches
-            step_kernel_ms[k] = step_kernel_ms.get(k, 0.0) + ms
-            step_kernel_n[k] = step_kernel_n.get(k, 0) + n
+        step()      # asynchronous: the next step's host setup overlaps this step's kernels
     torch.cuda.synchronize(local)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(local)
     elapsed = time.perf_counter() - t0
+    # per-kernel device times of the K timed steps (HIP events recorded on the launch stream)
+    kt = r.kernel_times()
+    step_kernel_ms = {k: v[0] for k, v in kt.items() if v[1]}
+    step_kernel_n = {k: v[1] for k, v in kt.items() if v[1]}
     r.enable_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -156,6 +177,8 @@ def main():
     samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
     value = samples_per_step * args.steps / elapsed / 1e6
 
+    workload = "frame %d, %dx%d, %d spp, %d bounces" % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel,
+                                                         cfg.max_bounces)
     result = None
     if rank == 0:
         roof = None
@@ -179,8 +202,11 @@ def main():
             achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9
             path_ms = sum(step_kernel_ms[k] for k in step_kernel_ms if k != "accumulate") / args.steps
             path_bytes = algorithmic_bytes(total)
+            traffic, traffic_src = pmc_traffic("extend", workload)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "traffic_source": traffic_src and ("%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                                                       "this workload, per launch)" % traffic_src),
                     "kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)",
                     "ms_per_launch": round(ms_per_launch, 4), "launches_per_step": ext_n / args.steps,
                     "bytes_per_launch": int(bytes_per_launch),
@@ -201,7 +227,7 @@ def main():
                 cpu = {"value": None, "unit": "Msamples/s", "cores": None, "kind": "reference",
                        "sample": "failed: %s" % str(e)[:300]}
         result = {
-            "metric": "Msamples/sec (whole node) at 1280x720 256spp, frame 0",
+            "metric": "Msamples/sec (whole node) at 1280x720 1024spp",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -213,8 +239,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene assets + deterministic substitutes, frame %d" % args.frame,
-            "config": {"workload": "frame %d, %dx%d, %d spp, %d bounces (BASELINE configs[1])"
-                                   % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel, cfg.max_bounces),
+            "config": {"workload": workload + " (BASELINE metric config)",
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
             "roofline": roof,
             "cpu_baseline": cpu,

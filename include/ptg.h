@@ -233,10 +233,14 @@ int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
 /* Counters split by kernel kind (same kinds as ptg_last_kernel_times). */
 int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
 
-/* Per-launch timing of the path-tracing kernel (k_trace), measured with HIP
- * events on the context's stream.  After enabling, each ptg_render* call
- * records its launches; ptg_last_timing returns their summed device time and
- * count (waits for the last launch). */
+/* Per-launch device timing, measured with HIP events recorded around every
+ * kernel launch on the context's stream.  Enabling (re)starts the record;
+ * every ptg_render* call after that appends its launches, without blocking
+ * the host, so host work (e.g. the next frame's setup) keeps overlapping the
+ * GPU.  Reading the record (ptg_last_timing / ptg_last_kernel_times) waits
+ * for the recorded launches, returns their summed device time and count, and
+ * clears it.  ptg_last_timing sums all path-tracing kernels (all kinds but
+ * accumulate). */
 int ptg_timing_enable(ptg_context* ctx, int enable);
 int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches);
 /* The same per kernel kind: [0] megakernel, [1] extend (closest-hit walk),

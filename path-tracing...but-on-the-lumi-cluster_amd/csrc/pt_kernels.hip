@@ -589,7 +589,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const DevScene sc = ctx->scene_args(cfg);
     const uint32_t persistent = ctx->persistent_blocks;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
-    ctx->ev_used = 0;
     for(uint32_t j = j0; j < j1; j += chunk)
     {
         const uint32_t nj = std::min(chunk, j1 - j);
@@ -1066,6 +1065,7 @@ int ptg_timing_enable(ptg_context* ctx, int enable)
 {
     if(!ctx) return fail(PTG_E_INVALID, "null context");
     ctx->timing = enable != 0;
+    ctx->ev_used = 0;
     return PTG_OK;
 }
 
@@ -1082,6 +1082,7 @@ int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8])
         ms[ctx->ev_kind[i]] += t;
         launches[ctx->ev_kind[i]] += 1;
     }
+    ctx->ev_used = 0;
     return PTG_OK;
 }
 

@@ -138,7 +138,7 @@ class GpuRenderer:
         N.check(N.lib().ptg_timing_enable(self._ctx, 1 if on else 0), "ptg_timing_enable")
 
     def last_timing(self):
-        """(summed k_trace device ms, launch count) of the last render call."""
+        """(summed path-kernel device ms, launch count) since timing was enabled or last read."""
         ms, n = C.c_double(), C.c_uint32()
         N.check(N.lib().ptg_last_timing(self._ctx, C.byref(ms), C.byref(n)), "ptg_last_timing")
         return ms.value, n.value
@@ -146,7 +146,8 @@ class GpuRenderer:
     KINDS = ("megakernel", "extend", "shadow", "shade", "camera", "accumulate")
 
     def kernel_times(self):
-        """{kind: (device ms, launches)} of the last render call (timing enabled)."""
+        """{kind: (device ms, launches)} summed over the launches recorded since
+        timing was enabled or last read (waits for them; clears the record)."""
         ms = np.zeros(8, np.float64)
         n = np.zeros(8, np.uint32)
         N.check(N.lib().ptg_last_kernel_times(self._ctx, ms.ctypes.data, n.ctypes.data), "ptg_last_kernel_times")
