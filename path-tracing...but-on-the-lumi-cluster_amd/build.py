@@ -25,6 +25,8 @@ REF_CONFIGS = [
     ("strict", 1280, 720, 256, 4),   # bench workload: per-sample spot checks
     ("v3", 1280, 720, 16, 4),        # CPU baseline (reference flags, portable -march)
 ]
+# reference host code + ptg_render in place of baseline_render (oracle/dropin_main.cc)
+DROPIN_CONFIGS = [("strict", 160, 90, 32, 4)]
 
 
 def _run(cmd, cwd, verbose):
@@ -49,6 +51,9 @@ def build_oracle(verbose=False, jobs=8, with_reference=None):
     if with_reference:
         for mode, w, h, spp, b in REF_CONFIGS:
             _run(["make", "-j%d" % jobs, "ref", "REF_MODE=%s" % mode, "REF_W=%d" % w, "REF_H=%d" % h,
+                  "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
+        for mode, w, h, spp, b in DROPIN_CONFIGS:   # needs libptg.so: build_native first
+            _run(["make", "-j%d" % jobs, "dropin", "REF_MODE=%s" % mode, "REF_W=%d" % w, "REF_H=%d" % h,
                   "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
 
 

@@ -65,7 +65,8 @@ def test_validator_psnr_against_reference_frame(full_frame):
     """validator.py's check: 2x-downscaled frame vs output/frame_0000.bmp.
     The reference image was made by its authors with fast-math (and with
     original terrain/bunny/tree assets the reference repository does not
-    ship - see DESIGN.md), so the comparison is statistical; the
+    ship - see DESIGN.md), and it is a 640x360 render while the validator
+    downscales our 1280x720 frame, so the comparison is statistical; the
     reference accepts >= 32 dB."""
     ref = np.load(os.path.join(GOLDEN, "frame_0000_ref.npz"))["rgb"]
     p, good = V.validate_frame(ref, full_frame[2])
@@ -132,3 +133,21 @@ def test_frame_sequence_through_scene_handle(gpu, assets_dir):
             assert np.array_equal(_bits(got[:, :3]), _bits(want[:, :3])), f
     finally:
         r.close()
+
+
+def test_reference_frame_0000_same_config(gpu, assets_dir):
+    """output/frame_0000.bmp is the reference's 640x360 x 256 spp TESTING
+    render of frame 0.  Rendered at that same configuration the
+    GPU frame must match it to within fast-math noise: SURVEY measured ~63 dB
+    for a correct renderer on the substitute scene, below ~50 dB means a
+    semantic bug (RNG, camera, tonemap, BGRA order)."""
+    s = scene_for(assets_dir, 640, 360, 256, frame=0)
+    gpu.upload_arrays(arrays_copy(s))
+    bgra, _ = gpu.render(s.cfg)
+    gpu.synchronize()
+    own = V.bgra_to_rgb(bgra.cpu().numpy())
+    ref = np.load(os.path.join(GOLDEN, "frame_0000_ref.npz"))["rgb"]
+    p = V.psnr(ref, own)
+    exact = float((own == ref).all(-1).mean())
+    print("frame 0 640x360x256 vs output/frame_0000.bmp: %.2f dB, %.1f%% pixels byte-exact" % (p, 100 * exact))
+    assert p >= 50.0 and exact > 0.8
