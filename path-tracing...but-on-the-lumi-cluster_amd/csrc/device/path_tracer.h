@@ -32,7 +32,7 @@ constexpr int SECONDARY_ITERATIONS = 4;
 
 // Work counters (only in the counting build of a kernel).
 struct Counters {
-    uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0;
+    uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0;
 };
 
 struct Hit {
@@ -116,7 +116,7 @@ struct Walker {
         }
         float4 lo, hi;
         load_trav((axis < 0 ? sc.tlas_trav : sc.blas_trav) + base + node, lo, hi);
-        if(COUNT) cnt.visits++;
+        if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; }
         // slab test (ray_query.hh:197-207); min/max results only feed compares
         const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
         const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;

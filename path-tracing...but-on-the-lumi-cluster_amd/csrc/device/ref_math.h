@@ -62,12 +62,21 @@ PTG_D float signf(float v)
 }
 
 // double-precision library calls, as the reference makes them
+#ifdef PTG_ABLATE_FASTMATH   // timing ablation only: single-precision hardware approximations
+PTG_D double dexp(double x) { return __expf((float)x); }
+PTG_D double dlog(double x) { return __logf((float)x); }
+PTG_D double dpow(double x, double y) { return __powf((float)x, (float)y); }
+PTG_D double dsin(double x) { return __sinf((float)x); }
+PTG_D double dcos(double x) { return __cosf((float)x); }
+PTG_D double dsqrt(double x) { return __fsqrt_rn((float)x); }
+#else
 PTG_D double dexp(double x) { return exp(x); }
 PTG_D double dlog(double x) { return log(x); }
 PTG_D double dpow(double x, double y) { return pow(x, y); }
 PTG_D double dsin(double x) { return sin(x); }
 PTG_D double dcos(double x) { return cos(x); }
 PTG_D double dsqrt(double x) { return sqrt(x); }
+#endif
 PTG_D float fcos(float x) { return (float)dcos((double)x); }
 PTG_D float fsin(float x) { return (float)dsin((double)x); }
 PTG_D float fexp(float x) { return (float)dexp((double)x); }

@@ -19,10 +19,12 @@
 #include "device/path_tracer.h"
 #include "device/wavefront.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 #include <unordered_set>
 #include <vector>
 
@@ -123,10 +125,11 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
 // Counting builds only: wave-reduce the counters, one atomic per counter per wave.
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* dev, uint32_t samples)
 {
-    const unsigned long long v[6] = {wave_sum(samples), wave_sum(c.visits), wave_sum(c.tri_tests),
-                                     wave_sum(c.blas_entries), wave_sum(c.queries), wave_sum(c.shades)};
+    const unsigned long long v[7] = {wave_sum(samples), wave_sum(c.visits), wave_sum(c.tri_tests),
+                                     wave_sum(c.blas_entries), wave_sum(c.queries), wave_sum(c.shades),
+                                     wave_sum(c.tlas_visits)};
     if((threadIdx.x & 63u) == 0)
-        for(int k = 0; k < 6; ++k)
+        for(int k = 0; k < 7; ++k)
             if(v[k]) atomicAdd(dev + k, v[k]);
 }
 
@@ -191,21 +194,31 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
 constexpr int kRefillIdle = 16;   // refill once at least this many lanes are idle
+#ifndef PTG_XCD_BANDS
+#define PTG_XCD_BANDS 1024
+#endif
+constexpr uint32_t kBands = PTG_XCD_BANDS;   // a multiple of the XCD count (8 on MI355X)
 
 template<bool ANY, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, const uint32_t* __restrict__ counts,
                                                     uint32_t round, const uint32_t* __restrict__ list, TraceOut tr,
-                                                    unsigned long long* __restrict__ counters)
+                                                    uint32_t nxcd, unsigned long long* __restrict__ counters)
 {
     const uint32_t n = counts[2 * round + (ANY ? 1 : 0)];
     const uint32_t lane = threadIdx.x & 63u;
-    // wave w takes the 64-entry groups w, w + W, w + 2W, ... of the queue: every
-    // wave samples the whole image (balanced), each group is 8 pixels x 8
-    // samples (coherent)
-    const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // XCD-aware static split: the queue's 64-entry groups (8 pixels x 8
+    // samples each) are cut into kBands bands dealt round-robin to the XCDs
+    // (workgroup b runs on XCD b % nxcd), so each XCD's L2 serves a few image
+    // bands instead of the whole frame.  Inside its bands, wave w of an XCD
+    // takes the groups w, w + W, w + 2W, ...: every wave samples all of its
+    // XCD's bands (balanced) and the waves in flight cover a narrow window.
+    const uint32_t xcd = blockIdx.x % nxcd;
+    const uint32_t waves = ((gridDim.x / nxcd) * blockDim.x) >> 6;
+    const uint32_t wave = ((blockIdx.x / nxcd) * blockDim.x + threadIdx.x) >> 6;
     const uint32_t groups = (n + 63u) >> 6;
-    const uint32_t end = wave < groups ? ((groups - wave + waves - 1) / waves) * 64u : 0u;
+    const uint32_t band = max(1u, (groups + kBands - 1u) / kBands);
+    const uint32_t local = (kBands / nxcd) * band;    // this XCD's group slots (some past the end)
+    const uint32_t end = wave < local ? ((local - wave + waves - 1) / waves) * 64u : 0u;
     uint32_t cursor = 0;
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
@@ -224,7 +237,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, cons
                 if(!active)
                 {
                     const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                    const uint32_t t = (wave + (v >> 6) * waves) * 64u + (v & 63u);
+                    const uint32_t l = wave + (v >> 6) * waves;
+                    const uint32_t t = ((xcd + nxcd * (l / band)) * band + l % band) * 64u + (v & 63u);
                     if(v < end && t < n)
                     {
                         q = ANY ? list[t] : t;
@@ -466,7 +480,9 @@ struct ptg_context {
     // 0: wavefront pipeline (default), 1: megakernel
     int pipeline = 0;
     uint32_t persistent_blocks = 2048;
-    uint32_t walk_grid[2] = {2048, 2048};   // resident blocks of k_wf_walk<closest/any>
+    uint32_t walk_grid[2] = {2048, 2048};
+    uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
+    uint32_t chunk_log2 = 28;              // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2)   // resident blocks of k_wf_walk<closest/any>
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
     ~ptg_context()
@@ -541,10 +557,22 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     if(j1 <= j0) return fail(PTG_E_INVALID, "empty sample range");
     const bool wf = ctx->pipeline == 0;
     // samples per chunk: megakernel <= 1 GiB of results; wavefront ~16 M live paths
-    const size_t target = wf ? (size_t(1) << 24) : ((size_t(1) << 30) / sizeof(float4));
-    uint32_t chunk = uint32_t(std::max<size_t>(8, target / size_t(pm.npix)));
-    chunk = std::min<uint32_t>(chunk & ~7u, j1 - j0);
-    if(chunk == 0) chunk = std::min<uint32_t>(8, j1 - j0);
+    // Wavefront chunks are as large as HBM allows (capped at 35% of it): every
+    // bounce round then launches over a long queue, so the walk and shade
+    // launches run at full occupancy with short tails.  2^28 paths = 93 GB.
+    size_t target = (size_t(1) << 30) / sizeof(float4);
+    if(wf)
+    {
+        size_t free_b = 0, total_b = 0;
+        PTG_HIP(hipMemGetInfo(&free_b, &total_b));
+        const size_t per_path = 2 * 9 * 16 + (16 + 16 + 4) + 2 * 4 + sizeof(float4);
+        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * 35 / per_path));
+    }
+    // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
+    const uint32_t span = j1 - j0;
+    const uint32_t max_chunk = std::max<uint32_t>(8, uint32_t(std::min<size_t>(target / size_t(pm.npix), span)) & ~7u);
+    const uint32_t nchunks = (span + max_chunk - 1) / max_chunk;
+    uint32_t chunk = std::min<uint32_t>(span, ((span + nchunks - 1) / nchunks + 7) & ~7u);
     const size_t M = size_t((pm.npix + 7) / 8) * ((chunk + 7) / 8) * 64;   // lanes per chunk (upper bound)
     if(M >= (1ull << 31)) return fail(PTG_E_RANGE, "chunk too large");
     PTG_HIP(ctx->samples.reserve(size_t(pm.npix) * chunk * sizeof(float4)));
@@ -626,10 +654,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 if(int e = timed_begin(ctx, K_EXTEND)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
-                                       counts, r, nullptr, tr, cnt_for(K_EXTEND));
+                                       counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
                 else
                     hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
-                                       counts, r, nullptr, tr, nullptr);
+                                       counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
                 if(r > 0)
@@ -637,10 +665,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     if(int e = timed_begin(ctx, K_SHADOW)) return e;
                     if(ctx->counting)
                         hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
-                                           cur, counts, r, lists[r & 1], tr, cnt_for(K_SHADOW));
+                                           cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
                     else
                         hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
-                                           cur, counts, r, lists[r & 1], tr, nullptr);
+                                           cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
                     PTG_HIP(hipGetLastError());
                     if(int e = timed_end(ctx)) return e;
                 }
@@ -654,6 +682,15 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
             }
+        }
+        if(wf && getenv("PTG_DEBUG_QUEUES"))
+        {   // diagnostics: per-round queue sizes of this chunk
+            std::vector<uint32_t> h(2 * (rounds + 2));
+            PTG_HIP(hipMemcpyAsync(h.data(), counts, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+            PTG_HIP(hipStreamSynchronize(ctx->stream));
+            fprintf(stderr, "chunk j=%u nj=%u lanes=%zu counts:", j, nj, lanes);
+            for(uint32_t v: h) fprintf(stderr, " %u", v);
+            fprintf(stderr, "\n");
         }
         const int first = j == j0, last = j + nj >= j1;
         if(int r = timed_begin(ctx, K_ACCUM)) return r;
@@ -742,6 +779,7 @@ int ptg_context_create(int device, ptg_context** out)
     ctx->counting = cnt && cnt[0] == '1';
     const char* pipe = getenv("PTG_PIPELINE");
     if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
+    if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(28, std::max(16, atoi(c))));
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 8;
     // the walk kernels split their queue statically over the waves of the grid,
     // so the grid must be exactly what is resident at once
@@ -750,6 +788,8 @@ int ptg_context_create(int device, ptg_context** out)
         ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, 0) == hipSuccess && per_cu > 0)
         ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
+    for(int k = 0; k < 2; ++k)
+        ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
     *out = ctx.release();
     return PTG_OK;
