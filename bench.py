@@ -38,23 +38,31 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# rocprofv3 PMC summary of this same workload (tools/profile_gpu.sh + tools/summarize_prof.py)
-TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_wavefront", "pmc_summary.json")
+PROFILES = os.path.join(ROOT, "profiles")
 
 
-def pmc_traffic(kind, workload):
-    """HBM-side bytes per launch of `kind` from the committed PMC passes
-    (FETCH_SIZE x 1 KiB x 2 per the gfx950 correction + WRITE_SIZE x 1 KiB),
-    or None when the profile is missing or was taken on another workload."""
-    try:
-        with open(TRAFFIC_PROFILE) as f:
-            prof = json.load(f)
-        if prof.get("_workload") != workload:
-            return None, None
-        d = prof[kind]["derived"]
-        return int(d["hbm_side_bytes"]), os.path.relpath(TRAFFIC_PROFILE, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+def pmc_traffic(kind, workload, ms_per_launch):
+    """HBM-side bytes per launch of `kind` from committed rocprofv3 PMC passes
+    of this same workload and code (tools/profile_gpu.sh + summarize_prof.py):
+    FETCH_SIZE x 1 KiB x 2 (gfx950 correction) + WRITE_SIZE x 1 KiB.  A
+    profile counts only if its kernel-trace average launch time agrees with the
+    live measurement within 15% (a profile of older code or another chunking
+    is not used); None when no profile qualifies."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(PROFILES, "*", "pmc_summary.json"))):
+        try:
+            with open(f) as fh:
+                prof = json.load(fh)
+            ent = prof[kind]
+            if prof.get("_workload") != workload or "hbm_side_bytes" not in ent["derived"]:
+                continue
+            if abs(ent["trace_avg_ms"] - ms_per_launch) > 0.15 * ms_per_launch:
+                continue
+            best = (int(ent["derived"]["hbm_side_bytes"]), os.path.relpath(f, ROOT))
+        except (OSError, KeyError, ValueError, TypeError):
+            continue
+    return best if best else (None, None)
 
 
 def algorithmic_bytes(c):
@@ -214,7 +222,7 @@ def main():
             achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9
             path_ms = sum(step_kernel_ms[k] for k in step_kernel_ms if k != "accumulate") / args.steps
             path_bytes = algorithmic_bytes(total)
-            traffic, traffic_src = pmc_traffic("extend", workload)
+            traffic, traffic_src = pmc_traffic("extend", workload, ms_per_launch)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "traffic_source": traffic_src and ("%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "

@@ -194,13 +194,18 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
 constexpr int kRefillIdle = 16;   // refill once at least this many lanes are idle
+#ifdef PTG_WALK_WAVES
+#define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PTG_WALK_WAVES, 8)))
+#else
+#define PTG_WALK_ATTR
+#endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
 #endif
 constexpr uint32_t kBands = PTG_XCD_BANDS;   // a multiple of the XCD count (8 on MI355X)
 
 template<bool ANY, bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_wf_walk(DevScene sc, PathSoA S, const uint32_t* __restrict__ counts,
+__global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, PathSoA S, const uint32_t* __restrict__ counts,
                                                     uint32_t round, const uint32_t* __restrict__ list, TraceOut tr,
                                                     uint32_t nxcd, unsigned long long* __restrict__ counters)
 {
