@@ -276,6 +276,14 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     if(COUNT) flush_counters(cnt, counters, 0);
 }
 
+// Shade one round's queue.  Each block takes 256 consecutive entries and
+// first regroups them through LDS by what their shading will run - surface
+// hit or sky, pending NEE to finish or not - so that a wave executes one of
+// the (long, mutually exclusive) branches of shade_path instead of all of
+// them; which lane shades which path has no effect on the result.
+#ifndef PTG_SHADE_BINS
+#define PTG_SHADE_BINS 1
+#endif
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
                                                      uint32_t round, TraceOut tr, uint32_t* __restrict__ next_list,
@@ -283,29 +291,57 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 {
     const uint32_t n = counts[2 * round];
     Counters cnt;
-    for(uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x)
+    __shared__ uint32_t bin_count[4];
+    __shared__ uint32_t perm[kBlock];
+    for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
     {
-        PathRec p = load_path(cur, q);
-        const uint4 hv = tr.hit[q];
-        const float4 bv = tr.bary[q];
-        Hit h;
-        h.thit = __uint_as_float(hv.x);
-        h.instance_id = hv.y;
-        h.primitive_id = hv.z;
-        h.back_face = hv.w != 0;
-        h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
-        const bool occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
-        const bool cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
-        const bool nee = cont && meta_nee(p.meta);
-#ifdef PTG_ABLATE_NO_APPEND
-        const uint32_t qn = q, sn = q;   // timing experiment only: no compaction
-        if(q == 0) { counts[2 * (round + 1)] = n; counts[2 * (round + 1) + 1] = n; }
-#else
+        uint32_t q = base + threadIdx.x;
+#if PTG_SHADE_BINS
+        if(threadIdx.x < 4) bin_count[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t key = 0, rank = 0;
+        if(q < n)
+        {
+            const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
+            const bool nee = round > 0 && meta_nee(cur.meta[q]) && tr.shadow[q] == 0;
+            key = (hit ? 2u : 0u) | (nee ? 1u : 0u);
+            rank = atomicAdd(&bin_count[key], 1u);
+        }
+        __syncthreads();
+        if(q < n)
+        {
+            uint32_t start = 0;
+            for(uint32_t k = 0; k < key; ++k) start += bin_count[k];
+            perm[start + rank] = q;
+        }
+        __syncthreads();
+        const uint32_t valid = min(n - base, (uint32_t)kBlock);
+        q = threadIdx.x < valid ? perm[threadIdx.x] : n;
+#endif
+        bool cont = false, nee = false;
+        PathRec p;
+        if(q < n)
+        {
+            p = load_path(cur, q);
+            const uint4 hv = tr.hit[q];
+            const float4 bv = tr.bary[q];
+            Hit h;
+            h.thit = __uint_as_float(hv.x);
+            h.instance_id = hv.y;
+            h.primitive_id = hv.z;
+            h.back_face = hv.w != 0;
+            h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
+            const bool occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
+            cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
+            nee = cont && meta_nee(p.meta);
+        }
         const uint32_t qn = wave_append(&counts[2 * (round + 1)], cont);
         const uint32_t sn = wave_append(&counts[2 * (round + 1) + 1], nee);
-#endif
         if(cont) store_path(nxt, qn, p);
         if(nee) next_list[sn] = qn;
+#if PTG_SHADE_BINS
+        __syncthreads();   // perm / bin_count are rewritten by the next iteration
+#endif
     }
     if(COUNT) flush_counters(cnt, counters, 0);
 }
