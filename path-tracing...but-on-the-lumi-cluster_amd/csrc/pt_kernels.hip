@@ -284,6 +284,9 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
 #ifndef PTG_SHADE_BINS
 #define PTG_SHADE_BINS 1
 #endif
+#ifndef PTG_SORT_APPEND
+#define PTG_SORT_APPEND 1
+#endif
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
                                                      uint32_t round, TraceOut tr, uint32_t* __restrict__ next_list,
@@ -293,6 +296,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
     Counters cnt;
     __shared__ uint32_t bin_count[4];
     __shared__ uint32_t perm[kBlock];
+    __shared__ uint32_t oct_count[8], oct_start[8], blk_base, nee_total, nee_base;
     for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
     {
         uint32_t q = base + threadIdx.x;
@@ -335,12 +339,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
             cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
             nee = cont && meta_nee(p.meta);
         }
+#if PTG_SORT_APPEND
+        // block-level append: one atomic per queue per block, survivors stored
+        // contiguously and grouped by the octant of their next ray, so the next
+        // round's 64-ray groups mostly walk one of the 8 link orders
+        if(threadIdx.x < 8) oct_count[threadIdx.x] = 0;
+        if(threadIdx.x == 8) nee_total = 0;
+        __syncthreads();
+        const uint32_t okey = cont ? octant(p.ray_d) : 0u;
+        const uint32_t orank = cont ? atomicAdd(&oct_count[okey], 1u) : 0u;
+        const uint32_t nrank = nee ? atomicAdd(&nee_total, 1u) : 0u;
+        __syncthreads();
+        if(threadIdx.x == 0)
+        {
+            uint32_t total = 0;
+            for(int k = 0; k < 8; ++k) { oct_start[k] = total; total += oct_count[k]; }
+            blk_base = total ? atomicAdd(&counts[2 * (round + 1)], total) : 0u;
+            nee_base = nee_total ? atomicAdd(&counts[2 * (round + 1) + 1], nee_total) : 0u;
+        }
+        __syncthreads();
+        const uint32_t qn = blk_base + oct_start[okey] + orank;
+        const uint32_t sn = nee_base + nrank;
+#else
         const uint32_t qn = wave_append(&counts[2 * (round + 1)], cont);
         const uint32_t sn = wave_append(&counts[2 * (round + 1) + 1], nee);
+#endif
         if(cont) store_path(nxt, qn, p);
         if(nee) next_list[sn] = qn;
-#if PTG_SHADE_BINS
-        __syncthreads();   // perm / bin_count are rewritten by the next iteration
+#if PTG_SHADE_BINS || PTG_SORT_APPEND
+        __syncthreads();   // the LDS tables are rewritten by the next iteration
 #endif
     }
     if(COUNT) flush_counters(cnt, counters, 0);
