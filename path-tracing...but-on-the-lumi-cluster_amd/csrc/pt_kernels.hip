@@ -193,7 +193,10 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the grid is sized to what is resident, each wave owns a contiguous range of
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
-constexpr int kRefillIdle = 16;   // refill once at least this many lanes are idle
+#ifndef PTG_REFILL_IDLE
+#define PTG_REFILL_IDLE 16
+#endif
+constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many lanes are idle
 #ifdef PTG_WALK_WAVES
 #define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PTG_WALK_WAVES, 8)))
 #else
