@@ -172,15 +172,17 @@ struct Walker {
         y = y - S.y * z;
         const f3 uvw = cross(y, x);
         const float det = uvw.x + uvw.y + uvw.z;
+        // the division-free parts of the acceptance test first: most tested
+        // triangles fail them, and those lanes then skip the IEEE division
+        if(!(det != 0.0f && ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
+                             (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f))))
+            return 0;
         const float rdet = 1.0f / det;
         const float u = uvw.x * rdet, v = uvw.y * rdet, t = dot(uvw, S.z * z) * rdet;
         bool back = det < 0;
         if(S.z < 0) back = !back;
         if(axis != 2) back = !back;
-        const bool hit = det != 0.0f && t >= 0.0f &&
-                         ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
-                          (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f));
-        if(hit && t < tmax && t > tmin)
+        if(t >= 0.0f && t < tmax && t > tmin)
         {
             if(ANY) return 2;
             // ray_query_confirm (ray_query.hh:280-290)
