@@ -859,6 +859,9 @@ int ptg_context_create(int device, ptg_context** out)
         ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, 0) == hipSuccess && per_cu > 0)
         ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
+    if(const char* w = getenv("PTG_WALK_BLOCKS_PER_CU"))   // experiments: fewer resident walk blocks
+        for(int k = 0; k < 2; ++k)
+            ctx->walk_grid[k] = std::min(ctx->walk_grid[k], uint32_t(std::max(1, atoi(w)) * prop.multiProcessorCount));
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
