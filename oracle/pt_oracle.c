@@ -18,7 +18,7 @@
  *   - literals such as `1.0 - p` are double;
  *   - fminf/fmaxf keep their tie rule (equal operands -> second operand).
  * Pinned against the reference itself built strict (oracle/Makefile
- * REF_MODE=strict): tests/test_oracle_vs_reference.py requires bit-identical
+ * REF_MODE=strict): tests/test_oracle.py requires bit-identical
  * per-sample output.  The GPU kernel (csrc/pt_kernels.hip) is checked
  * against this file.
  */
