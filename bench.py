@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--tile", type=str, default="32x16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--animation", type=int, default=0, metavar="K",
+                    help="also render K frames spread evenly over the whole animation (frame-parallel over the "
+                         "ranks) and report frames/min for the full animation (BASELINE config 4)")
     args = ap.parse_args()
 
     import numpy as np
@@ -193,6 +196,36 @@ def main():
     # (2) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
     elapsed_frame, _ = timed(frame_step, False)
 
+    anim = None
+    if args.animation > 0:
+        # BASELINE config 4: the animation frame-parallel over the ranks, one frame
+        # per GPU at a time; K frames spread evenly over all 1800 (frame cost varies ~7x)
+        total_frames = scene.frame_count()
+        picks = [round(i * total_frames / args.animation) % total_frames for i in range(args.animation)]
+        mine = picks[rank::world]
+        torch.cuda.synchronize(local)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for f in mine:
+            scene.setup_frame(f)
+            r.upload(scene, include_static=False)
+            r.render(cfg, out_bgra=image)
+        torch.cuda.synchronize(local)
+        if world > 1:
+            dist.barrier()
+        anim_s = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([anim_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            anim_s = float(t.item())
+        anim = {"frames_per_min": round(len(picks) / anim_s * 60.0, 3),
+                "full_animation_min": round(total_frames / (len(picks) / anim_s * 60.0), 2),
+                "msamples_per_s": round(len(picks) * cfg.width * cfg.height * cfg.samples_per_pixel / anim_s / 1e6, 3),
+                "frames": len(picks), "frame_stride": total_frames // max(1, args.animation),
+                "seconds": round(anim_s, 3),
+                "step": "setup_animation_frame + per-frame upload + render per frame, frames dealt to ranks round-robin"}
+
     samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
     value = samples_per_step * args.steps / elapsed / 1e6
     value_frame = samples_per_step * args.steps / elapsed_frame / 1e6
@@ -261,6 +294,7 @@ def main():
             "data": "synthetic: reference scene assets + deterministic substitutes, frame %d" % args.frame,
             "config": {"workload": workload + " (BASELINE metric config)",
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
+            "animation": anim,
             "with_frame_setup": {"value": round(value_frame, 3), "unit": "Msamples/s",
                                  "ms_per_step": round(elapsed_frame / args.steps * 1e3, 3),
                                  "step": "setup_animation_frame (host) + per-frame H2D upload + render, "
