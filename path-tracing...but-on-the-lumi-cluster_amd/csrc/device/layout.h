@@ -23,13 +23,25 @@
 
 namespace ptg {
 
+#ifndef PTG_PAIR_NODES
+#define PTG_PAIR_NODES 1
+#endif
 struct alignas(16) TravRec {
     float min_x, min_y, min_z;
     uint32_t accept;           // top bit: leaf; payload in the low 31 bits
     float max_x, max_y, max_z;
     uint32_t cancel;           // next node when the box is missed / after a leaf
+#if PTG_PAIR_NODES
+    // The same fields of node `cancel` in the same link order (cancel2 =
+    // 0xFFFFFFFF when `cancel` ends the walk): a step whose box is missed
+    // tests the next node right away instead of a dependent load later.
+    float min2_x, min2_y, min2_z;
+    uint32_t accept2;
+    float max2_x, max2_y, max2_z;
+    uint32_t cancel2;
+#endif
 };
-static_assert(sizeof(TravRec) == 32, "TravRec is two 16-byte loads");
+static_assert(sizeof(TravRec) == 32 * (1 + PTG_PAIR_NODES), "TravRec is two (four) 16-byte loads");
 
 struct alignas(16) TriRec {
     float p0x, p0y, p0z, p1x;

@@ -97,6 +97,17 @@ struct Walker {
         best.back_face = false;
     }
 
+    // slab test (ray_query.hh:197-207); min/max results only feed compares
+    PTG_D bool box_hit(float4 lo, float4 hi) const
+    {
+        const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
+        const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;
+        const float t0z = (lo.z - org.z) * inv.z, t1z = (hi.z - org.z) * inv.z;
+        const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
+        const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
+        return nearv <= farv && farv > tmin && nearv < tmax;
+    }
+
     // One step.  Returns 0 while the walk goes on, 1 when it has ended, 2 (ANY
     // only) when an occluder was found.
     template<bool ANY, bool COUNT>
@@ -115,16 +126,29 @@ struct Walker {
             return 0;
         }
         float4 lo, hi;
-        load_trav((axis < 0 ? sc.tlas_trav : sc.blas_trav) + base + node, lo, hi);
+        const TravRec* rec = (axis < 0 ? sc.tlas_trav : sc.blas_trav) + base + node;
+        load_trav(rec, lo, hi);
+#if PTG_PAIR_NODES
+        const float4* rq = reinterpret_cast<const float4*>(rec);
+        const float4 lo2 = rq[2], hi2 = rq[3];
+#endif
         if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; }
-        // slab test (ray_query.hh:197-207); min/max results only feed compares
-        const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
-        const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;
-        const float t0z = (lo.z - org.z) * inv.z, t1z = (hi.z - org.z) * inv.z;
-        const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
-        const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
-        const uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
-        if(!(nearv <= farv && farv > tmin && nearv < tmax)) { node = cancel; return 0; }
+        uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
+        if(!box_hit(lo, hi))
+        {
+#if PTG_PAIR_NODES
+            // missed: the next node in link order is `cancel`, whose record came
+            // with this one - test it now, exactly as the next step would
+            if(cancel >= count) { node = cancel; return 0; }
+            if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; }
+            accept = __float_as_uint(lo2.w);
+            cancel = __float_as_uint(hi2.w);
+            if(!box_hit(lo2, hi2)) { node = cancel; return 0; }
+#else
+            node = cancel;
+            return 0;
+#endif
+        }
         if(!(accept & 0x80000000u)) { node = accept; return 0; }
         node = cancel;
         const uint32_t leaf = accept & 0x7FFFFFFFu;

@@ -64,6 +64,21 @@ __global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh
         TravRec r;
         r.min_x = n.min_x; r.min_y = n.min_y; r.min_z = n.min_z; r.accept = l.accept;
         r.max_x = n.max_x; r.max_y = n.max_y; r.max_z = n.max_z; r.cancel = l.cancel;
+#if PTG_PAIR_NODES
+        if(l.cancel < j.count)
+        {
+            const uint32_t c = l.cancel;
+            const ptg_bvh_node n2 = nodes[j.node_begin + c];
+            const ptg_bvh_link l2 = links[j.link_begin + (k - i) + c];   // same link order
+            r.min2_x = n2.min_x; r.min2_y = n2.min_y; r.min2_z = n2.min_z; r.accept2 = l2.accept;
+            r.max2_x = n2.max_x; r.max2_y = n2.max_y; r.max2_z = n2.max_z; r.cancel2 = l2.cancel;
+        }
+        else
+        {
+            r.min2_x = r.min2_y = r.min2_z = 0.0f; r.accept2 = 0xFFFFFFFFu;
+            r.max2_x = r.max2_y = r.max2_z = 0.0f; r.cancel2 = 0xFFFFFFFFu;
+        }
+#endif
         out[j.out_begin + k] = r;
     }
 }
