@@ -874,6 +874,12 @@ int ptg_context_create(int device, ptg_context** out)
         ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, 0) == hipSuccess && per_cu > 0)
         ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
+    // 4 x the resident grid: each block's static share is a quarter, and the
+    // dispatcher starts the later blocks as earlier ones retire, which trims
+    // the launch tail (measured: extend -2% on frame 0, -3.5% on frame 450)
+    uint32_t oversub = 4;
+    if(const char* w = getenv("PTG_WALK_OVERSUB")) oversub = uint32_t(std::max(1, atoi(w)));
+    for(int k = 0; k < 2; ++k) ctx->walk_grid[k] *= oversub;
     if(const char* w = getenv("PTG_WALK_BLOCKS_PER_CU"))   // experiments: fewer resident walk blocks
         for(int k = 0; k < 2; ++k)
             ctx->walk_grid[k] = std::min(ctx->walk_grid[k], uint32_t(std::max(1, atoi(w)) * prop.multiProcessorCount));
