@@ -867,8 +867,8 @@ int ptg_context_create(int device, ptg_context** out)
     if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
     if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(28, std::max(16, atoi(c))));
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 8;
-    // the walk kernels split their queue statically over the waves of the grid,
-    // so the grid must be exactly what is resident at once
+    // walk grids: a multiple of what is resident at once (the queue is split
+    // statically over the waves of the whole grid)
     int per_cu = 0;
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, 0) == hipSuccess && per_cu > 0)
         ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
