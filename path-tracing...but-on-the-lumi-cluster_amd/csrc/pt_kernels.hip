@@ -866,7 +866,9 @@ int ptg_context_create(int device, ptg_context** out)
     const char* pipe = getenv("PTG_PIPELINE");
     if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
     if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(28, std::max(16, atoi(c))));
-    ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 8;
+    uint32_t per_cu_blocks = 32;   // grid-stride kernels (camera, shade): measured best of 3..128
+    if(const char* w = getenv("PTG_BLOCKS_PER_CU")) per_cu_blocks = uint32_t(std::max(1, atoi(w)));
+    ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * per_cu_blocks;
     // walk grids: a multiple of what is resident at once (the queue is split
     // statically over the waves of the whole grid)
     int per_cu = 0;
