@@ -244,7 +244,8 @@ int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
 int ptg_timing_enable(ptg_context* ctx, int enable);
 int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches);
 /* The same per kernel kind: [0] megakernel, [1] extend (closest-hit walk),
- * [2] shadow (any-hit walk), [3] shade, [4] camera, [5] accumulate. */
+ * [2] shadow (any-hit walk), [3] shade (surface hits), [4] camera,
+ * [5] accumulate, [6] sky (rays that left the scene), [7] classify. */
 int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8]);
 
 /* Execution strategy of ptg_render*: 0 = wavefront pipeline (default:

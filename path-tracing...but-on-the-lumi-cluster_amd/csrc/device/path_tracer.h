@@ -259,13 +259,15 @@ PTG_D float4 ld4(const float* base, uint32_t i) { return reinterpret_cast<const 
 
 // The shading half of trace_ray (path_tracer.hh:351-411): turn the closest
 // hit of the ray (origin, dir) into a hit_info.
-template<bool COUNT>
+// KIND: 0 = either, 1 = the caller knows the ray hit, 2 = it knows it missed
+// (lets the wavefront kernels compile only the branch they run).
+template<bool COUNT, int KIND = 0>
 PTG_D HitInfo hit_info(const DevScene& sc, const Light& L, f3 origin, f3 dir, const Hit& h, Counters& cnt)
 {
     HitInfo hi;
     hi.thit = h.thit;
     hi.nee_pdf = 0;
-    if(hi.thit < 0)
+    if(KIND == 2 || (KIND == 0 && hi.thit < 0))
     {
         const float visible = dot(L.dir, dir) > L.cos ? 1.0f : 0.0f;
         hi.nee_pdf = visible / (2.0f * PI_F * (1.0f - L.cos));

@@ -113,7 +113,10 @@ PTG_D uint4 to_uint4(u4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 // Shade one queued path after its current ray was traced (and its pending
 // NEE ray, if any, tested).  Returns true when the path continues; `next` is
 // then the state for the next round.
-template<bool COUNT>
+//
+// KIND as in hit_info: the sky kernel instantiates KIND = 2 (the path's ray
+// missed, so the path ends here), the surface kernel KIND = 1.
+template<bool COUNT, int KIND = 0>
 PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occluded, float4* out_samples,
                       Counters& cnt)
 {
@@ -122,7 +125,7 @@ PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occlude
     const Light L = light_of(sf);
     const uint32_t round = meta_round(p.meta);
     u4 seed = to_u4(p.seed);
-    HitInfo info = hit_info<COUNT>(sc, L, p.ray_o, p.ray_d, h, cnt);
+    HitInfo info = hit_info<COUNT, KIND>(sc, L, p.ray_o, p.ray_d, h, cnt);
     if(round == 0)
     {   // primary ray (path_tracer.hh:686-693)
         f3 attenuation, in_scatter;
@@ -138,7 +141,7 @@ PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occlude
         p.contrib = p.contrib + p.att * nee;
         bounce_tail(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg);
     }
-    if(!(round < sc.max_bounces && info.thit > 0))
+    if(KIND == 2 || !(round < sc.max_bounces && info.thit > 0))
     {
         out_samples[p.meta.x] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f);
         return false;

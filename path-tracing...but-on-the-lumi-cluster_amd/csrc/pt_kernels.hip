@@ -294,73 +294,107 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     if(COUNT) flush_counters(cnt, counters, 0);
 }
 
-// Shade one round's queue.  Each block takes 256 consecutive entries and
-// first regroups them through LDS by what their shading will run - surface
-// hit or sky, pending NEE to finish or not - so that a wave executes one of
-// the (long, mutually exclusive) branches of shade_path instead of all of
-// them; which lane shades which path has no effect on the result.
-#ifndef PTG_SHADE_BINS
-#define PTG_SHADE_BINS 1
-#endif
-#ifndef PTG_SORT_APPEND
-#define PTG_SORT_APPEND 1
-#endif
-template<bool COUNT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts,
-                                                     uint32_t round, TraceOut tr, uint32_t* __restrict__ next_list,
-                                                     float4* __restrict__ out, unsigned long long* __restrict__ counters)
+// Shading of one round is split by what the paths will run.
+//
+// k_wf_classify reads every queued path's trace result and deals the queue,
+// 256 entries per block, into two lists through an LDS counting sort: paths
+// whose ray hit a surface (shaded by k_wf_shade) and paths whose ray left the
+// scene (shaded by k_wf_sky), each grouped by whether a pending NEE ray still
+// has to be finished.  A wave then runs one of the long, mutually exclusive
+// branches of shade_path, and the sky branch - the double-precision
+// atmosphere integrals - runs in its own small kernel at high occupancy.
+// Which lane shades which path has no effect on the result.
+__global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
+                                                        const uint4* __restrict__ meta, uint32_t* __restrict__ hit_list,
+                                                        uint32_t* __restrict__ sky_list, uint32_t* __restrict__ lcounts)
 {
+    // Each block deals a tile of kTile entries with ONE 64-bit atomic on the
+    // packed (hit, sky) list lengths: a device-scope atomic is a fabric round
+    // trip serialized per address, so their number, not the bytes, sets this
+    // kernel's time.
+    constexpr uint32_t kSub = 8, kTile = kSub * kBlock;
     const uint32_t n = counts[2 * round];
-    Counters cnt;
     __shared__ uint32_t bin_count[4];
-    __shared__ uint32_t perm[kBlock];
+    __shared__ unsigned long long base2;
+    for(uint32_t tile = blockIdx.x * kTile; tile < n; tile += gridDim.x * kTile)
+    {
+        if(threadIdx.x < 4) bin_count[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t key[kSub], rank[kSub];
+#pragma unroll
+        for(uint32_t k = 0; k < kSub; ++k)
+        {
+            const uint32_t q = tile + k * kBlock + threadIdx.x;
+            key[k] = 4u;
+            rank[k] = 0;
+            if(q < n)
+            {
+                const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
+                const bool nee = round > 0 && meta_nee(meta[q]) && tr.shadow[q] == 0;
+                key[k] = (hit ? 2u : 0u) | (nee ? 1u : 0u);
+                rank[k] = atomicAdd(&bin_count[key[k]], 1u);
+            }
+        }
+        __syncthreads();
+        if(threadIdx.x == 0)
+        {
+            const unsigned long long nsky = bin_count[0] + bin_count[1], nhit = bin_count[2] + bin_count[3];
+            base2 = atomicAdd(reinterpret_cast<unsigned long long*>(lcounts), (nsky << 32) | nhit);
+        }
+        __syncthreads();
+        const uint32_t hit_base = uint32_t(base2), sky_base = uint32_t(base2 >> 32);
+#pragma unroll
+        for(uint32_t k = 0; k < kSub; ++k)
+        {
+            const uint32_t q = tile + k * kBlock + threadIdx.x;
+            if(key[k] == 4u) continue;
+            if(key[k] & 2u) hit_list[hit_base + (key[k] == 3u ? bin_count[2] : 0u) + rank[k]] = q;
+            else sky_list[sky_base + (key[k] == 1u ? bin_count[0] : 0u) + rank[k]] = q;
+        }
+        __syncthreads();   // bin_count is rewritten by the next tile
+    }
+}
+
+__device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& tr, uint32_t q, PathRec& p, Hit& h,
+                                            bool& occluded)
+{
+    p = load_path(cur, q);
+    const uint4 hv = tr.hit[q];
+    const float4 bv = tr.bary[q];
+    h.thit = __uint_as_float(hv.x);
+    h.instance_id = hv.y;
+    h.primitive_id = hv.z;
+    h.back_face = hv.w != 0;
+    h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
+    occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
+}
+
+// Surface hits: NEE finish, bounce tail, then NEE setup + BSDF sample of the
+// next bounce or retire.  Survivors are appended per block (one atomic per
+// queue per block), stored contiguously and grouped by the octant of their
+// next ray, so the next round's 64-ray groups mostly walk one link order.
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(
+    DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
+    const uint32_t* __restrict__ hit_list, const uint32_t* __restrict__ lcounts, uint32_t* __restrict__ next_list,
+    float4* __restrict__ out, unsigned long long* __restrict__ counters)
+{
+    const uint32_t n = lcounts[0];
+    Counters cnt;
     __shared__ uint32_t oct_count[8], oct_start[8], blk_base, nee_total, nee_base;
     for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
     {
-        uint32_t q = base + threadIdx.x;
-#if PTG_SHADE_BINS
-        if(threadIdx.x < 4) bin_count[threadIdx.x] = 0;
-        __syncthreads();
-        uint32_t key = 0, rank = 0;
-        if(q < n)
-        {
-            const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
-            const bool nee = round > 0 && meta_nee(cur.meta[q]) && tr.shadow[q] == 0;
-            key = (hit ? 2u : 0u) | (nee ? 1u : 0u);
-            rank = atomicAdd(&bin_count[key], 1u);
-        }
-        __syncthreads();
-        if(q < n)
-        {
-            uint32_t start = 0;
-            for(uint32_t k = 0; k < key; ++k) start += bin_count[k];
-            perm[start + rank] = q;
-        }
-        __syncthreads();
-        const uint32_t valid = min(n - base, (uint32_t)kBlock);
-        q = threadIdx.x < valid ? perm[threadIdx.x] : n;
-#endif
+        const uint32_t i = base + threadIdx.x;
         bool cont = false, nee = false;
         PathRec p;
-        if(q < n)
+        if(i < n)
         {
-            p = load_path(cur, q);
-            const uint4 hv = tr.hit[q];
-            const float4 bv = tr.bary[q];
             Hit h;
-            h.thit = __uint_as_float(hv.x);
-            h.instance_id = hv.y;
-            h.primitive_id = hv.z;
-            h.back_face = hv.w != 0;
-            h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
-            const bool occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
-            cont = shade_path<COUNT>(sc, p, h, occluded, out, cnt);
+            bool occluded;
+            load_queued(cur, tr, hit_list[i], p, h, occluded);
+            cont = shade_path<COUNT, 1>(sc, p, h, occluded, out, cnt);
             nee = cont && meta_nee(p.meta);
         }
-#if PTG_SORT_APPEND
-        // block-level append: one atomic per queue per block, survivors stored
-        // contiguously and grouped by the octant of their next ray, so the next
-        // round's 64-ray groups mostly walk one of the 8 link orders
         if(threadIdx.x < 8) oct_count[threadIdx.x] = 0;
         if(threadIdx.x == 8) nee_total = 0;
         __syncthreads();
@@ -369,24 +403,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         const uint32_t nrank = nee ? atomicAdd(&nee_total, 1u) : 0u;
         __syncthreads();
         if(threadIdx.x == 0)
-        {
-            uint32_t total = 0;
-            for(int k = 0; k < 8; ++k) { oct_start[k] = total; total += oct_count[k]; }
-            blk_base = total ? atomicAdd(&counts[2 * (round + 1)], total) : 0u;
-            nee_base = nee_total ? atomicAdd(&counts[2 * (round + 1) + 1], nee_total) : 0u;
+        {   // one 64-bit atomic on the packed (queue, NEE list) lengths
+            unsigned long long total = 0;
+            for(int k = 0; k < 8; ++k) { oct_start[k] = uint32_t(total); total += oct_count[k]; }
+            const unsigned long long old =
+                (total | nee_total)
+                    ? atomicAdd(reinterpret_cast<unsigned long long*>(&counts[2 * (round + 1)]),
+                                (uint64_t(nee_total) << 32) | total)
+                    : 0ull;
+            blk_base = uint32_t(old);
+            nee_base = uint32_t(old >> 32);
         }
         __syncthreads();
         const uint32_t qn = blk_base + oct_start[okey] + orank;
-        const uint32_t sn = nee_base + nrank;
-#else
-        const uint32_t qn = wave_append(&counts[2 * (round + 1)], cont);
-        const uint32_t sn = wave_append(&counts[2 * (round + 1) + 1], nee);
-#endif
         if(cont) store_path(nxt, qn, p);
-        if(nee) next_list[sn] = qn;
-#if PTG_SHADE_BINS || PTG_SORT_APPEND
+        if(nee) next_list[nee_base + nrank] = qn;
         __syncthreads();   // the LDS tables are rewritten by the next iteration
-#endif
+    }
+    if(COUNT) flush_counters(cnt, counters, 0);
+}
+
+// Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
+// (path_tracer.hh:456-588), retire.  No survivors.
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr,
+                                                   const uint32_t* __restrict__ sky_list,
+                                                   const uint32_t* __restrict__ lcounts, float4* __restrict__ out,
+                                                   unsigned long long* __restrict__ counters)
+{
+    const uint32_t n = lcounts[1];
+    Counters cnt;
+    for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    {
+        PathRec p;
+        Hit h;
+        bool occluded;
+        load_queued(cur, tr, sky_list[i], p, h, occluded);
+        shade_path<COUNT, 2>(sc, p, h, occluded, out, cnt);
     }
     if(COUNT) flush_counters(cnt, counters, 0);
 }
@@ -628,7 +681,10 @@ int check_cfg(const ptg_context* ctx, const ptg_render_config* cfg, uint32_t sam
 }
 
 // Kernel kinds for timing and work counters.
-enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA = 4, K_ACCUM = 5, K_KINDS = 6 };
+// (work counters use the first K_KINDS; the sky and classify kernels are timed
+// separately and count into K_SHADE)
+enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA = 4, K_ACCUM = 5, K_KINDS = 6,
+                  K_SKY = 6, K_CLASSIFY = 7 };
 
 int timed_begin(ptg_context* ctx, int kind);
 int timed_end(ptg_context* ctx);
@@ -651,7 +707,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     {
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
-        const size_t per_path = 2 * 9 * 16 + (16 + 16 + 4) + 2 * 4 + sizeof(float4);
+        const size_t per_path = 2 * 9 * 16 + (16 + 16 + 4) + 4 * 4 + sizeof(float4);
         target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * 35 / per_path));
     }
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
@@ -674,12 +730,13 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     PathSoA S[2];
     TraceOut tr{};
     uint32_t* lists[2] = {nullptr, nullptr};
+    uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
     uint32_t* counts = nullptr;
     if(wf)
     {
         // path state: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
         const size_t rec = M * 16;
-        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + M * (16 + 16 + 4) + 2 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
         char* b = ctx->wf_state.as<char>();
         for(int h = 0; h < 2; ++h)
         {
@@ -698,6 +755,8 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         tr.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
         lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
         lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        sky_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
         counts = reinterpret_cast<uint32_t*>(b);
     }
     const DevScene sc = ctx->scene_args(cfg);
@@ -758,13 +817,28 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     PTG_HIP(hipGetLastError());
                     if(int e = timed_end(ctx)) return e;
                 }
+                uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
+                if(int e = timed_begin(ctx, K_CLASSIFY)) return e;
+                hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ctx->stream, counts, r, tr, cur.meta, hit_list,
+                                   sky_list, lc);
+                PTG_HIP(hipGetLastError());
+                if(int e = timed_end(ctx)) return e;
                 if(int e = timed_begin(ctx, K_SHADE)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
-                                       lists[(r + 1) & 1], out, cnt_for(K_SHADE));
+                                       hit_list, lc, lists[(r + 1) & 1], out, cnt_for(K_SHADE));
                 else
                     hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
-                                       lists[(r + 1) & 1], out, nullptr);
+                                       hit_list, lc, lists[(r + 1) & 1], out, nullptr);
+                PTG_HIP(hipGetLastError());
+                if(int e = timed_end(ctx)) return e;
+                if(int e = timed_begin(ctx, K_SKY)) return e;
+                if(ctx->counting)
+                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, tr, sky_list, lc, out,
+                                       cnt_for(K_SHADE));
+                else
+                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, tr, sky_list, lc, out,
+                                       nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
             }
@@ -1231,7 +1305,8 @@ int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches)
     if(int r = ptg_last_kernel_times(ctx, ms, n)) return r;
     *trace_ms = 0;
     *launches = 0;
-    for(int k = 0; k < K_ACCUM; ++k) { *trace_ms += ms[k]; *launches += n[k]; }
+    for(int k = 0; k < 8; ++k)
+        if(k != K_ACCUM) { *trace_ms += ms[k]; *launches += n[k]; }
     return PTG_OK;
 }
 

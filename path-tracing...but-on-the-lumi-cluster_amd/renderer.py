@@ -143,7 +143,7 @@ class GpuRenderer:
         N.check(N.lib().ptg_last_timing(self._ctx, C.byref(ms), C.byref(n)), "ptg_last_timing")
         return ms.value, n.value
 
-    KINDS = ("megakernel", "extend", "shadow", "shade", "camera", "accumulate")
+    KINDS = ("megakernel", "extend", "shadow", "shade", "camera", "accumulate", "sky", "classify")
 
     def kernel_times(self):
         """{kind: (device ms, launches)} summed over the launches recorded since
@@ -157,7 +157,7 @@ class GpuRenderer:
         """{kind: counters[8]} of the last render call (counting enabled)."""
         out = np.zeros((6, 8), np.uint64)
         N.check(N.lib().ptg_last_kernel_counters(self._ctx, out.ctypes.data), "ptg_last_kernel_counters")
-        return {k: out[i] for i, k in enumerate(self.KINDS)}
+        return {k: out[i] for i, k in enumerate(self.KINDS[:6])}
 
     def set_pipeline(self, name):
         """'wavefront' (default) or 'megakernel' - bit-identical results."""
