@@ -217,6 +217,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #else
 #define PTG_WALK_ATTR
 #endif
+#ifndef PTG_WALK_UNROLL
+#define PTG_WALK_UNROLL 2   // walk steps per refill check (measured: 2 beats 1 and 3)
+#endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
 #endif
@@ -275,6 +278,8 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             }
         }
         if(!__any(active)) break;
+#pragma unroll
+        for(int u = 0; u < PTG_WALK_UNROLL; ++u)
         if(active)
         {
             const int r = w.template step<ANY, COUNT>(sc, cnt);
@@ -425,8 +430,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
 // (path_tracer.hh:456-588), retire.  No survivors.
+#ifdef PTG_SKY_WAVES
+#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
+#else
+#define PTG_SKY_ATTR
+#endif
 template<bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr,
+__global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr,
                                                    const uint32_t* __restrict__ sky_list,
                                                    const uint32_t* __restrict__ lcounts, float4* __restrict__ out,
                                                    unsigned long long* __restrict__ counters)
