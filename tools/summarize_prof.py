@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 KERNELS = {"extend": "k_wf_walk<false, false>", "shadow": "k_wf_walk<true, false>", "shade": "k_wf_shade<false>",
-           "camera": "k_wf_camera<false>", "accumulate": "k_accumulate", "megakernel": "k_trace<false>"}
+           "camera": "k_wf_camera<false>", "accumulate": "k_accumulate", "megakernel": "k_trace<false>",
+           "sky": "k_wf_sky<false>", "classify": "k_wf_classify"}
 
 
 def derive(avg, trace_avg_ns):
@@ -56,7 +57,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--workload", default="frame 0, 1280x720, 1024 spp, 4 bounces",
                     help="bench workload the profile was taken on (bench.py reads traffic only on a match)")
-    ap.add_argument("--kernels", default="extend,shadow,shade,camera,accumulate",
+    ap.add_argument("--kernels", default="extend,shadow,shade,sky,classify,camera,accumulate",
                     help="comma list of " + ",".join(KERNELS))
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles", a.tag)
