@@ -132,9 +132,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    # PTG_BENCH_REHEARSE=1: rehearse the N>1 code paths with more ranks than GPUs
+    # (ranks share devices, gloo instead of RCCL, which cannot put two ranks on
+    # one GPU); never used for a measurement
+    rehearse = os.environ.get("PTG_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     assets = os.path.join(ROOT, "assets")
     cfg = N.RenderConfig.make(args.width, args.height, args.spp, args.bounces)
@@ -183,7 +192,7 @@ def main():
         kt = r.kernel_times() if timing else {}
         r.enable_timing(False)
         if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearse else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el, kt
@@ -216,7 +225,7 @@ def main():
             dist.barrier()
         anim_s = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([anim_s], dtype=torch.float64, device=dev)
+            t = torch.tensor([anim_s], dtype=torch.float64, device="cpu" if rehearse else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             anim_s = float(t.item())
         anim = {"frames_per_min": round(len(picks) / anim_s * 60.0, 3),

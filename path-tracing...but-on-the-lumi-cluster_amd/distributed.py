@@ -106,6 +106,11 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None):
                               out_bgra=buf[:shard.count * per_tile])
     if shard.world == 1:
         parts = [buf]
+    elif dist.get_backend() == "gloo":   # CPU process groups (tests, rehearsals): gather through host memory
+        host = buf.cpu()
+        hparts = [torch.empty_like(host) for _ in range(shard.world)] if shard.rank == 0 else None
+        dist.gather(host, hparts, dst=0)
+        parts = [p.to(dev) for p in hparts] if shard.rank == 0 else None
     else:
         parts = [torch.empty_like(buf) for _ in range(shard.world)] if shard.rank == 0 else None
         dist.gather(buf, parts, dst=0)
