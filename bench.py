@@ -216,11 +216,15 @@ def main():
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for f in mine:
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(mine) + 1)]
+        marks[0].record(stream)
+        for k, f in enumerate(mine):
             scene.setup_frame(f)
             r.upload(scene, include_static=False)
             r.render(cfg, out_bgra=image)
+            marks[k + 1].record(stream)
         torch.cuda.synchronize(local)
+        per_frame = sorted(((marks[k].elapsed_time(marks[k + 1]), f) for k, f in enumerate(mine)), reverse=True)
         if world > 1:
             dist.barrier()
         anim_s = time.perf_counter() - t0
@@ -233,6 +237,7 @@ def main():
                 "msamples_per_s": round(len(picks) * cfg.width * cfg.height * cfg.samples_per_pixel / anim_s / 1e6, 3),
                 "frames": len(picks), "frame_stride": total_frames // max(1, args.animation),
                 "seconds": round(anim_s, 3),
+                "slowest_frames_ms": [[f, round(ms, 1)] for ms, f in per_frame[:5]],
                 "step": "setup_animation_frame + per-frame upload + render per frame, frames dealt to ranks round-robin"}
 
     samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
