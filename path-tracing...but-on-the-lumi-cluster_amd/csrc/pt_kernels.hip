@@ -634,8 +634,14 @@ struct ptg_context {
     uint32_t chunk_log2 = 28;              // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2)   // resident blocks of k_wf_walk<closest/any>
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
+    // second stream for the sky kernels + the events that order it with `stream`
+    hipStream_t side = nullptr;
+    hipEvent_t ev_main = nullptr, ev_side = nullptr;
     ~ptg_context()
     {
+        if(ev_main) (void)hipEventDestroy(ev_main);
+        if(ev_side) (void)hipEventDestroy(ev_side);
+        if(side) (void)hipStreamDestroy(side);
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
         for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
     }
@@ -696,8 +702,8 @@ int check_cfg(const ptg_context* ctx, const ptg_render_config* cfg, uint32_t sam
 enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA = 4, K_ACCUM = 5, K_KINDS = 6,
                   K_SKY = 6, K_CLASSIFY = 7 };
 
-int timed_begin(ptg_context* ctx, int kind);
-int timed_end(ptg_context* ctx);
+int timed_begin(ptg_context* ctx, int kind, hipStream_t st = nullptr);
+int timed_end(ptg_context* ctx, hipStream_t st = nullptr);
 
 // Render the pixels of `pm` for samples [j0, j1): per chunk of samples, the
 // path kernels write one float4 per (pixel, sample); k_accumulate folds the
@@ -717,7 +723,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     {
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
-        const size_t per_path = 2 * 9 * 16 + (16 + 16 + 4) + 4 * 4 + sizeof(float4);
+        const size_t per_path = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 4 * 4 + sizeof(float4);
         target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * 35 / per_path));
     }
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
@@ -738,7 +744,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     }
     const uint32_t rounds = cfg->max_bounces + 1;
     PathSoA S[2];
-    TraceOut tr{};
+    TraceOut trs[2] = {};   // per round parity: the sky kernel of round r reads its set while round r+1 writes the other
     uint32_t* lists[2] = {nullptr, nullptr};
     uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
     uint32_t* counts = nullptr;
@@ -746,7 +752,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     {
         // path state: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
         const size_t rec = M * 16;
-        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
         char* b = ctx->wf_state.as<char>();
         for(int h = 0; h < 2; ++h)
         {
@@ -760,9 +766,12 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             S[h].nee_c = reinterpret_cast<float4*>(b); b += rec;
             S[h].nee_d = reinterpret_cast<float4*>(b); b += rec;
         }
-        tr.hit = reinterpret_cast<uint4*>(b); b += M * 16;
-        tr.bary = reinterpret_cast<float4*>(b); b += M * 16;
-        tr.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        for(TraceOut& t: trs)
+        {
+            t.hit = reinterpret_cast<uint4*>(b); b += M * 16;
+            t.bary = reinterpret_cast<float4*>(b); b += M * 16;
+            t.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
+        }
         lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
         lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
         hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
@@ -771,6 +780,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     }
     const DevScene sc = ctx->scene_args(cfg);
     const uint32_t persistent = ctx->persistent_blocks;
+    const bool overlap = wf && ctx->side != nullptr;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
     for(uint32_t j = j0; j < j1; j += chunk)
     {
@@ -806,6 +816,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             {
                 const PathSoA& cur = S[r & 1];
                 const PathSoA& nxt = S[(r + 1) & 1];
+                const TraceOut& tr = trs[r & 1];
                 if(int e = timed_begin(ctx, K_EXTEND)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
@@ -828,6 +839,9 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     if(int e = timed_end(ctx)) return e;
                 }
                 uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
+                // the previous round's sky kernel (side stream) must be done with the
+                // lists and with the state set shade is about to overwrite
+                if(overlap && r > 0) PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
                 if(int e = timed_begin(ctx, K_CLASSIFY)) return e;
                 hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ctx->stream, counts, r, tr, cur.meta, hit_list,
                                    sky_list, lc);
@@ -842,16 +856,27 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                                        hit_list, lc, lists[(r + 1) & 1], out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
-                if(int e = timed_begin(ctx, K_SKY)) return e;
+                // escaped rays retire without feeding the next round: their
+                // double-precision atmosphere runs on a second stream, overlapping
+                // the next round's latency-bound walks
+                hipStream_t ss = ctx->stream;
+                if(overlap)
+                {
+                    PTG_HIP(hipEventRecord(ctx->ev_main, ctx->stream));
+                    PTG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+                    ss = ctx->side;
+                }
+                if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, tr, sky_list, lc, out,
+                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, sky_list, lc, out,
                                        cnt_for(K_SHADE));
                 else
-                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, tr, sky_list, lc, out,
-                                       nullptr);
+                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
-                if(int e = timed_end(ctx)) return e;
+                if(int e = timed_end(ctx, ss)) return e;
+                if(overlap) PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
             }
+            if(overlap) PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));   // join before accumulate
         }
         if(wf && getenv("PTG_DEBUG_QUEUES"))
         {   // diagnostics: per-round queue sizes of this chunk
@@ -888,7 +913,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     return PTG_OK;
 }
 
-int timed_begin(ptg_context* ctx, int kind)
+int timed_begin(ptg_context* ctx, int kind, hipStream_t st)
 {
     if(!ctx->timing) return PTG_OK;
     if(ctx->ev_used == ctx->ev_start.size())
@@ -901,14 +926,14 @@ int timed_begin(ptg_context* ctx, int kind)
         ctx->ev_kind.push_back(0);
     }
     ctx->ev_kind[ctx->ev_used] = kind;
-    PTG_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+    PTG_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], st ? st : ctx->stream));
     return PTG_OK;
 }
 
-int timed_end(ptg_context* ctx)
+int timed_end(ptg_context* ctx, hipStream_t st)
 {
     if(!ctx->timing) return PTG_OK;
-    PTG_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used++], ctx->stream));
+    PTG_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used++], st ? st : ctx->stream));
     return PTG_OK;
 }
 
@@ -972,6 +997,12 @@ int ptg_context_create(int device, ptg_context** out)
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
+    if(getenv("PTG_NO_OVERLAP") == nullptr)
+    {
+        PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
+        PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
+    }
     *out = ctx.release();
     return PTG_OK;
 }
