@@ -826,22 +826,29 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
+                // second stream: the previous round's sky kernel, then this round's
+                // shadow walk (independent of the closest-hit walk it runs beside)
+                hipStream_t ss = overlap ? ctx->side : ctx->stream;
                 if(r > 0)
                 {
-                    if(int e = timed_begin(ctx, K_SHADOW)) return e;
+                    if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
                     if(ctx->counting)
-                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), 0, ss, sc,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
                     else
-                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), 0, ctx->stream, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), 0, ss, sc,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
                     PTG_HIP(hipGetLastError());
-                    if(int e = timed_end(ctx)) return e;
+                    if(int e = timed_end(ctx, ss)) return e;
                 }
                 uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
-                // the previous round's sky kernel (side stream) must be done with the
-                // lists and with the state set shade is about to overwrite
-                if(overlap && r > 0) PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
+                // classify/shade need the shadow results, the lists the previous sky
+                // kernel read, and the state set it read
+                if(overlap)
+                {
+                    PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
+                    PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
+                }
                 if(int e = timed_begin(ctx, K_CLASSIFY)) return e;
                 hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ctx->stream, counts, r, tr, cur.meta, hit_list,
                                    sky_list, lc);
@@ -857,14 +864,12 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
                 // escaped rays retire without feeding the next round: their
-                // double-precision atmosphere runs on a second stream, overlapping
+                // double-precision atmosphere runs on the second stream, overlapping
                 // the next round's latency-bound walks
-                hipStream_t ss = ctx->stream;
                 if(overlap)
                 {
                     PTG_HIP(hipEventRecord(ctx->ev_main, ctx->stream));
                     PTG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
-                    ss = ctx->side;
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
@@ -874,9 +879,12 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
-                if(overlap) PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
             }
-            if(overlap) PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));   // join before accumulate
+            if(overlap)
+            {   // join before accumulate
+                PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
+                PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
+            }
         }
         if(wf && getenv("PTG_DEBUG_QUEUES"))
         {   // diagnostics: per-round queue sizes of this chunk
