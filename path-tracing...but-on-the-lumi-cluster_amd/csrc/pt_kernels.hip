@@ -51,27 +51,59 @@ struct BvhJob {
     uint32_t out_begin;    // first record in the output TravRec array
 };
 
+// Depth-first record order.  The walk visits nodes in each link order's
+// pre-order (accept = first child, cancel = next subtree), so each order's
+// records are stored in that order: after a hit the next node is the very next
+// record (same cache line), after a miss the walk jumps forward.  Node
+// identities, boxes and the link structure are unchanged - only addresses.
+// perm[link index] = position of the node in its order's pre-order walk
+// (0xFFFFFFFF for a node the walk cannot reach).  One thread per (BVH, order).
+constexpr uint32_t kUnreached = 0xFFFFFFFFu;
+
+__global__ void k_preorder(const ptg_bvh_link* __restrict__ links, uint32_t* __restrict__ perm,
+                           const BvhJob* __restrict__ jobs, uint32_t njobs)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if(t >= 8u * njobs) return;
+    const BvhJob j = jobs[t / 8u];
+    const uint32_t base = j.link_begin + (t % 8u) * j.count;
+    uint32_t n = 0, pos = 0;
+    while(n < j.count && pos < j.count)
+    {
+        perm[base + n] = pos++;
+        const ptg_bvh_link l = links[base + n];
+        n = (l.accept & 0x80000000u) ? l.cancel : l.accept;
+    }
+}
+
 __global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh_link* __restrict__ links,
-                           TravRec* __restrict__ out, const BvhJob* __restrict__ jobs)
+                           const uint32_t* __restrict__ perm, TravRec* __restrict__ out, const BvhJob* __restrict__ jobs)
 {
     const BvhJob j = jobs[blockIdx.y];
     const uint32_t total = 8u * j.count;
     for(uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x)
     {
-        const uint32_t i = k % j.count;
+        const uint32_t i = k % j.count, ob = k - i;     // node, first link of its order
+        const uint32_t p = perm[j.link_begin + k];
+        if(p == kUnreached) continue;
+        const uint32_t* pm = perm + j.link_begin + ob;
         const ptg_bvh_node n = nodes[j.node_begin + i];
         const ptg_bvh_link l = links[j.link_begin + k];
         TravRec r;
-        r.min_x = n.min_x; r.min_y = n.min_y; r.min_z = n.min_z; r.accept = l.accept;
-        r.max_x = n.max_x; r.max_y = n.max_y; r.max_z = n.max_z; r.cancel = l.cancel;
+        r.min_x = n.min_x; r.min_y = n.min_y; r.min_z = n.min_z;
+        r.accept = (l.accept & 0x80000000u) ? l.accept : pm[l.accept];
+        r.max_x = n.max_x; r.max_y = n.max_y; r.max_z = n.max_z;
+        r.cancel = l.cancel < j.count ? pm[l.cancel] : l.cancel;
 #if PTG_PAIR_NODES
         if(l.cancel < j.count)
         {
             const uint32_t c = l.cancel;
             const ptg_bvh_node n2 = nodes[j.node_begin + c];
-            const ptg_bvh_link l2 = links[j.link_begin + (k - i) + c];   // same link order
-            r.min2_x = n2.min_x; r.min2_y = n2.min_y; r.min2_z = n2.min_z; r.accept2 = l2.accept;
-            r.max2_x = n2.max_x; r.max2_y = n2.max_y; r.max2_z = n2.max_z; r.cancel2 = l2.cancel;
+            const ptg_bvh_link l2 = links[j.link_begin + ob + c];   // same link order
+            r.min2_x = n2.min_x; r.min2_y = n2.min_y; r.min2_z = n2.min_z;
+            r.accept2 = (l2.accept & 0x80000000u) ? l2.accept : pm[l2.accept];
+            r.max2_x = n2.max_x; r.max2_y = n2.max_y; r.max2_z = n2.max_z;
+            r.cancel2 = l2.cancel < j.count ? pm[l2.cancel] : l2.cancel;
         }
         else
         {
@@ -79,7 +111,7 @@ __global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh
             r.max2_x = r.max2_y = r.max2_z = 0.0f; r.cancel2 = 0xFFFFFFFFu;
         }
 #endif
-        out[j.out_begin + k] = r;
+        out[j.out_begin + ob + p] = r;
     }
 }
 
@@ -609,7 +641,7 @@ struct ptg_context {
     bool counting = false;
     // static scene (reference layout) + repacked records
     DevBuf nodes, links, indices, pos, normal, albedo, material;
-    DevBuf blas_trav, tris;
+    DevBuf blas_trav, tris, perm;
     size_t static_nodes = 0, index_count = 0, vertex_count = 0;
     std::unordered_set<uint32_t> packed_bvh, packed_mesh;
     bool scene_ready = false;
@@ -952,9 +984,20 @@ int pack_bvhs(ptg_context* ctx, const std::vector<BvhJob>& jobs, const ptg_bvh_n
     PTG_HIP(ctx->jobs.reserve(jobs.size() * sizeof(BvhJob)));
     PTG_HIP(hipMemcpyAsync(ctx->jobs.p, jobs.data(), jobs.size() * sizeof(BvhJob), hipMemcpyHostToDevice, ctx->stream));
     uint32_t maxc = 0;
-    for(const BvhJob& j: jobs) maxc = std::max(maxc, 8 * j.count);
+    size_t link_end = 0;
+    for(const BvhJob& j: jobs)
+    {
+        maxc = std::max(maxc, 8 * j.count);
+        link_end = std::max(link_end, size_t(j.link_begin) + size_t(8) * j.count);
+    }
+    PTG_HIP(ctx->perm.reserve(link_end * sizeof(uint32_t)));
+    PTG_HIP(hipMemsetAsync(ctx->perm.p, 0xFF, link_end * sizeof(uint32_t), ctx->stream));
+    hipLaunchKernelGGL(k_preorder, dim3(grid_for(8 * jobs.size(), 64)), dim3(64), 0, ctx->stream, links,
+                       ctx->perm.as<uint32_t>(), ctx->jobs.as<BvhJob>(), uint32_t(jobs.size()));
+    PTG_HIP(hipGetLastError());
     dim3 grid(std::min<uint32_t>(grid_for(maxc), 4096), uint32_t(jobs.size()));
-    hipLaunchKernelGGL(k_pack_bvh, grid, dim3(kBlock), 0, ctx->stream, nodes, links, out, ctx->jobs.as<BvhJob>());
+    hipLaunchKernelGGL(k_pack_bvh, grid, dim3(kBlock), 0, ctx->stream, nodes, links, ctx->perm.as<uint32_t>(), out,
+                       ctx->jobs.as<BvhJob>());
     PTG_HIP(hipGetLastError());
     PTG_HIP(hipStreamSynchronize(ctx->stream));   // jobs buffer is reused
     return PTG_OK;
