@@ -227,7 +227,8 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
  * on: ptg_counters_enable, or PTG_COUNTERS=1 at context creation; counting
  * uses a separate, slower build of the kernel):
  * [0] samples, [1] node visits, [2] triangle tests, [3] BLAS entries,
- * [4] ray queries, [5] closest-hit shades, [6] TLAS node visits (part of [1]). */
+ * [4] ray queries, [5] closest-hit shades, [6] TLAS node visits (part of [1]),
+ * [7] walk-loop iterations of whole waves (diagnostics). */
 int ptg_counters_enable(ptg_context* ctx, int enable);
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
 /* Counters split by kernel kind (same kinds as ptg_last_kernel_times). */

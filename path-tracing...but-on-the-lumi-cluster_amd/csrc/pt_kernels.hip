@@ -172,11 +172,11 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
 // Counting builds only: wave-reduce the counters, one atomic per counter per wave.
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* dev, uint32_t samples)
 {
-    const unsigned long long v[7] = {wave_sum(samples), wave_sum(c.visits), wave_sum(c.tri_tests),
+    const unsigned long long v[8] = {wave_sum(samples), wave_sum(c.visits), wave_sum(c.tri_tests),
                                      wave_sum(c.blas_entries), wave_sum(c.queries), wave_sum(c.shades),
-                                     wave_sum(c.tlas_visits)};
+                                     wave_sum(c.tlas_visits), wave_sum(c.iters)};
     if((threadIdx.x & 63u) == 0)
-        for(int k = 0; k < 7; ++k)
+        for(int k = 0; k < 8; ++k)
             if(v[k]) atomicAdd(dev + k, v[k]);
 }
 
@@ -310,6 +310,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             }
         }
         if(!__any(active)) break;
+        if(COUNT && lane == 0) cnt.iters++;   // wave loop iterations (lane 0 counts for its wave)
 #pragma unroll
         for(int u = 0; u < PTG_WALK_UNROLL; ++u)
         if(active)
