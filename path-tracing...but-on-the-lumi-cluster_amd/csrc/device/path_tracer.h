@@ -32,7 +32,7 @@ constexpr int SECONDARY_ITERATIONS = 4;
 
 // Work counters (only in the counting build of a kernel).
 struct Counters {
-    uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0;
+    uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0, iters = 0;
 };
 
 struct Hit {
