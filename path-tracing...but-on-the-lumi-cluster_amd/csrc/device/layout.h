@@ -64,8 +64,7 @@ static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
 
 // Everything a hot-path kernel reads, passed by value as a kernel argument.
 struct DevScene {
-    const TravRec* blas_trav;      // static BVH records (BLAS), index = global link index
-    const TravRec* tlas_trav;      // per-frame TLAS records, index = global link index - 8*first_frame_node
+    const TravRec* trav;           // BVH records of both levels, index = global link index
     const TriRec* tris;
     const InstTrav* inst_trav;
     const InstShade* inst_shade;
@@ -74,7 +73,6 @@ struct DevScene {
     const float* albedo;           // float4[]
     const float* material;         // float4[]
     const uint8_t* subframes;      // reference subframe[] (160 B each)
-    uint32_t tlas_link_base;       // 8 * first_frame_node
     uint32_t width, height, spp, max_bounces, student_id, blur_step;
     uint32_t subframe_count;
 };

@@ -79,7 +79,7 @@ struct Walker {
         tmin = t0;
         tmax = t1;
         tlas_count = tc;
-        tlas_base = to * 8 + octant(rd) * tc - sc.tlas_link_base;
+        tlas_base = to * 8 + octant(rd) * tc;
         org = o;
         inv = inv_w;
         base = tlas_base;
@@ -126,7 +126,7 @@ struct Walker {
             return 0;
         }
         float4 lo, hi;
-        const TravRec* rec = (axis < 0 ? sc.tlas_trav : sc.blas_trav) + base + node;
+        const TravRec* rec = sc.trav + (base + node);
         load_trav(rec, lo, hi);
 #if PTG_PAIR_NODES
         const float4* rq = reinterpret_cast<const float4*>(rec);

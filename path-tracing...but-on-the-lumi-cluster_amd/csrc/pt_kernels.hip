@@ -642,12 +642,12 @@ struct ptg_context {
     bool counting = false;
     // static scene (reference layout) + repacked records
     DevBuf nodes, links, indices, pos, normal, albedo, material;
-    DevBuf blas_trav, tris, perm;
+    DevBuf trav, tris, perm;   // trav: BLAS records then the frame's TLAS records, by global link index
     size_t static_nodes = 0, index_count = 0, vertex_count = 0;
     std::unordered_set<uint32_t> packed_bvh, packed_mesh;
     bool scene_ready = false;
     // frame
-    DevBuf frame_nodes, frame_links, tlas_trav, subframes, inst_trav, inst_shade, jobs;
+    DevBuf frame_nodes, frame_links, subframes, inst_trav, inst_shade, jobs;
     size_t first_frame_node = 0, frame_node_count = 0, subframe_count = 0, instance_count = 0;
     std::vector<ptg_subframe> host_subframes;
     bool frame_ready = false;
@@ -682,8 +682,7 @@ struct ptg_context {
     DevScene scene_args(const ptg_render_config* cfg) const
     {
         DevScene s;
-        s.blas_trav = blas_trav.as<TravRec>();
-        s.tlas_trav = tlas_trav.as<TravRec>();
+        s.trav = trav.as<TravRec>();
         s.tris = tris.as<TriRec>();
         s.inst_trav = inst_trav.as<InstTrav>();
         s.inst_shade = inst_shade.as<InstShade>();
@@ -692,7 +691,6 @@ struct ptg_context {
         s.albedo = albedo.as<float>();
         s.material = material.as<float>();
         s.subframes = subframes.as<uint8_t>();
-        s.tlas_link_base = uint32_t(8 * first_frame_node);
         s.width = cfg ? cfg->width : 0;
         s.height = cfg ? cfg->height : 0;
         s.spp = cfg ? cfg->samples_per_pixel : 0;
@@ -1093,7 +1091,6 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     PTG_HIP(ctx->normal.reserve(vertex_count * 16));
     PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
     PTG_HIP(ctx->material.reserve(vertex_count * 16));
-    PTG_HIP(ctx->blas_trav.reserve(8 * node_count * sizeof(TravRec)));
     PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec)));
     hipStream_t s = ctx->stream;
     PTG_HIP(hipMemcpyAsync(ctx->nodes.p, nodes, node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
@@ -1124,6 +1121,19 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
     if((first_node + frame_node_count) * 8 >= (1ull << 32)) return fail(PTG_E_RANGE, "ptg_upload_frame: too many nodes");
     ctx->frame_ready = false;
     hipStream_t s = ctx->stream;
+    // one record buffer for both levels, indexed by global link index (BLAS:
+    // static nodes, TLAS: this frame's nodes after them), so a walk step
+    // addresses either level through the same pointer; growing it drops the
+    // packed BLAS records, which are then repacked below
+    {
+        const size_t need = 8 * (first_node + frame_node_count) * sizeof(TravRec);
+        if(need > ctx->trav.bytes)
+        {
+            PTG_HIP(hipStreamSynchronize(s));
+            PTG_HIP(ctx->trav.reserve(need + need / 8));
+            ctx->packed_bvh.clear();
+        }
+    }
 
     // validate handles, pack instances, collect BLAS / mesh packing jobs
     std::vector<InstTrav> it(instance_count);
@@ -1171,7 +1181,7 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
            t.node_count == 0)
             return fail(PTG_E_RANGE, "subframe " + std::to_string(i) + ": TLAS outside the frame nodes");
         const uint32_t rel = uint32_t(t.node_offset - first_node);
-        tlas_jobs.push_back(BvhJob{rel, rel * 8, t.node_count, rel * 8});
+        tlas_jobs.push_back(BvhJob{rel, rel * 8, t.node_count, uint32_t(t.node_offset) * 8});   // global link index
         // every TLAS leaf must name a valid instance
     }
     for(size_t k = 0; k < 8 * frame_node_count; ++k)
@@ -1186,7 +1196,6 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
     PTG_HIP(ctx->subframes.reserve(subframe_count * sizeof(ptg_subframe)));
     PTG_HIP(ctx->frame_nodes.reserve(frame_node_count * sizeof(ptg_bvh_node)));
     PTG_HIP(ctx->frame_links.reserve(8 * frame_node_count * sizeof(ptg_bvh_link)));
-    PTG_HIP(ctx->tlas_trav.reserve(8 * frame_node_count * sizeof(TravRec)));
     PTG_HIP(hipMemcpyAsync(ctx->inst_trav.p, it.data(), instance_count * sizeof(InstTrav), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->inst_shade.p, is.data(), instance_count * sizeof(InstShade), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->subframes.p, subframes, subframe_count * sizeof(ptg_subframe), hipMemcpyHostToDevice, s));
@@ -1194,10 +1203,10 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
     PTG_HIP(hipMemcpyAsync(ctx->frame_links.p, frame_links, 8 * frame_node_count * sizeof(ptg_bvh_link),
                            hipMemcpyHostToDevice, s));
     if(int r = pack_bvhs(ctx, blas_jobs, ctx->nodes.as<ptg_bvh_node>(), ctx->links.as<ptg_bvh_link>(),
-                         ctx->blas_trav.as<TravRec>()))
+                         ctx->trav.as<TravRec>()))
         return r;
     if(int r = pack_bvhs(ctx, tlas_jobs, ctx->frame_nodes.as<ptg_bvh_node>(), ctx->frame_links.as<ptg_bvh_link>(),
-                         ctx->tlas_trav.as<TravRec>()))
+                         ctx->trav.as<TravRec>()))
         return r;
     if(!mesh_jobs.empty())
     {
