@@ -9,6 +9,7 @@
 #include "scene_internal.h"
 #include "hmath.h"
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -146,13 +147,6 @@ void play(AnimState& st, float t)
     }
 }
 
-std::pair<ptg_mesh, ptg_bvh>& load_pair(ptg_scene& s, const std::string& assets, const char* name)
-{
-    ptg_mesh m = load_obj_mesh(s.mesh_buf, assets + "/data/" + name + ".obj");
-    ptg_bvh b = build_blas(m, s.mesh_buf, s.bvh_buf);
-    return s.meshes[name] = {m, b};
-}
-
 void add_instance(ptg_scene& s, const char* name, const m4& transform)       // scene.cc:51-60
 {
     const auto& p = s.meshes.at(name);
@@ -189,9 +183,77 @@ bool terrain_trace(ptg_scene& s, const ptg_bvh& tlas, f3 origin, f3 dir, f3* hit
     return true;
 }
 
+// The meshes of load_scene (scene.cc:139-183), in load order.
+const char* const kMeshNames[] = {"terrain", "leaf_tree", "maple_tree", "pine_tree", "tropical_tree", "willow_tree",
+                                  "rock0", "rock1", "rock2", "rock3", "rock4", "armadillo", "buddha", "bunny",
+                                  "dragon", "teapot", "end", "logo"};
+
+// Parse + BLAS build of every mesh on worker threads, each into buffers of
+// its own, then appended in load order.  A mesh's arrays and its BVH (links
+// and leaf payloads are BVH-local indices) do not depend on what was loaded
+// before it, so appending with rebased offsets gives the very bytes of the
+// sequential load (tests/test_scene_parity.py).
+void load_meshes_parallel(ptg_scene& s, const std::string& assets)
+{
+    constexpr size_t kCount = sizeof(kMeshNames) / sizeof(kMeshNames[0]);
+    struct Part {
+        MeshBuffers mb;
+        BvhBuffers bb;
+        ptg_mesh m{};
+        ptg_bvh b{};
+        std::string error;
+    };
+    std::vector<Part> parts(kCount);
+    size_t threads = std::thread::hardware_concurrency();
+    if(const char* e = std::getenv("PTG_LOAD_THREADS")) threads = size_t(std::max(1, atoi(e)));
+    threads = std::max<size_t>(1, std::min<size_t>(threads ? threads : 1, std::min<size_t>(kCount, 16)));
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+        // biggest meshes are not first in the list; a shared counter balances them
+        for(size_t i; (i = next.fetch_add(1)) < kCount;)
+        {
+            Part& p = parts[i];
+            try
+            {
+                p.m = load_obj_mesh(p.mb, assets + "/data/" + kMeshNames[i] + ".obj");
+                p.b = build_blas(p.m, p.mb, p.bb);
+            }
+            catch(const std::exception& ex)
+            {
+                p.error = ex.what();
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for(size_t t = 1; t < threads; ++t) pool.emplace_back(worker);
+    worker();
+    for(std::thread& t: pool) t.join();
+    for(Part& p: parts)
+        if(!p.error.empty()) throw std::runtime_error(p.error);
+    for(size_t i = 0; i < kCount; ++i)
+    {
+        Part& p = parts[i];
+        MeshBuffers& mb = s.mesh_buf;
+        p.m.index_offset += uint32_t(mb.indices.size());
+        p.m.base_vertex_offset += uint32_t(mb.pos.size());
+        mb.indices.insert(mb.indices.end(), p.mb.indices.begin(), p.mb.indices.end());
+        mb.pos.insert(mb.pos.end(), p.mb.pos.begin(), p.mb.pos.end());
+        mb.normal.insert(mb.normal.end(), p.mb.normal.begin(), p.mb.normal.end());
+        mb.albedo.insert(mb.albedo.end(), p.mb.albedo.begin(), p.mb.albedo.end());
+        mb.material.insert(mb.material.end(), p.mb.material.begin(), p.mb.material.end());
+        BvhBuffers& bb = s.bvh_buf;
+        p.b.node_offset += uint32_t(bb.nodes.size());
+        bb.nodes.insert(bb.nodes.end(), p.bb.nodes.begin(), p.bb.nodes.end());
+        bb.links.insert(bb.links.end(), p.bb.links.begin(), p.bb.links.end());
+        s.meshes[kMeshNames[i]] = {p.m, p.b};
+        p = Part{};   // release the part's memory early
+    }
+}
+
 void load(ptg_scene& s, const std::string& assets)
 {
-    auto terrain = load_pair(s, assets, "terrain");
+    load_meshes_parallel(s, assets);
+    const auto terrain = s.meshes.at("terrain");
     const std::vector<GradientStop> albedo_gradient = {
         {-10, v4((float)0.25, (float)0.2, (float)0.1, 1)},
         {5, v4((float)0.2, (float)0.3, (float)0.02, 1)},
@@ -208,11 +270,6 @@ void load(ptg_scene& s, const std::string& assets)
         s.mesh_buf.albedo[i] = gradient(albedo_gradient, h);
         s.mesh_buf.material[i] = gradient(material_gradient, h);
     }
-    for(const char* name: {"leaf_tree", "maple_tree", "pine_tree", "tropical_tree", "willow_tree", "rock0", "rock1",
-                           "rock2", "rock3", "rock4", "armadillo", "buddha", "bunny", "dragon", "teapot", "end",
-                           "logo"})
-        load_pair(s, assets, name);
-
     add_instance(s, "terrain", v3(0, 0, 0), v3(0, 0, 0));
 
     // throwaway terrain-only TLAS for object placement (scene.cc:186-189)
