@@ -12,8 +12,8 @@
 //                   tris[index_offset/3 + t] (ray_query.hh:228-234 gathers
 //                   indices then positions: two dependent loads -> one).
 //   InstTrav  64 B  what ray_query_enter_blas needs (ray_query.hh:153-182):
-//                   inv_transform columns xyz of rows 0..3, BLAS handle and
-//                   the mesh's triangle base.
+//                   inv_transform rows 0..3 (xyz), each with one of the BLAS
+//                   handle and the mesh's triangle base in w.
 //   InstShade 64 B  what the closest-hit shading needs (path_tracer.hh:369-392):
 //                   transform rows 0..2 xyz and the mesh offsets.
 // BLAS records live in one buffer (uploaded once); the per-frame TLAS
@@ -51,8 +51,9 @@ struct alignas(16) TriRec {
 static_assert(sizeof(TriRec) == 48, "TriRec is three 16-byte loads");
 
 struct alignas(16) InstTrav {
-    float m[12];               // inv_transform.r[k].{x,y,z} for k = 0..3
-    uint32_t blas_count, blas_offset, tri_base, pad;
+    // row k = inv_transform.r[k].{x,y,z} in xyz; w = blas count, blas offset,
+    // triangle base, 0 for rows 0..3: four whole, aligned 16-byte loads
+    float4 row[4];
 };
 static_assert(sizeof(InstTrav) == 64, "InstTrav is four 16-byte loads");
 

@@ -156,18 +156,21 @@ struct Walker {
         {
             // ray_query_enter_blas (ray_query.hh:153-182)
             if(COUNT) cnt.blas_entries++;
-            const float4* ip = reinterpret_cast<const float4*>(sc.inst_trav + leaf);
-            const float4 a = ip[0], b = ip[1], c = ip[2], e = ip[3];
-            // a = M0.xyz M1.x | b = M1.yz M2.xy | c = M2.z M3.xyz | e = blas count, offset, tri_base
-            const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(a.w, b.x, b.y), M2 = V3(b.z, b.w, c.x), M3 = V3(c.y, c.z, c.w);
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + leaf);
+            // whole-row vector loads: float4 members get re-split by the
+            // compiler into unaligned pieces (5 loads instead of 4)
+            const v4f a = ip[0], b = ip[1], c = ip[2], e = ip[3];
+            // rows M0..M3 of inv_transform in xyz; w: blas count, offset, tri_base
+            const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(b.x, b.y, b.z), M2 = V3(c.x, c.y, c.z), M3 = V3(e.x, e.y, e.z);
             org = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
                      M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
                      M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
             const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
                              M0.y * d.x + M1.y * d.y + M2.y * d.z,
                              M0.z * d.x + M1.z * d.y + M2.z * d.z);
-            const uint32_t bcount = __float_as_uint(e.x), boffset = __float_as_uint(e.y);
-            tri_base = __float_as_uint(e.z);
+            const uint32_t bcount = __float_as_uint(a.w), boffset = __float_as_uint(b.w);
+            tri_base = __float_as_uint(c.w);
             inst = leaf;
             tlas_resume = node;
             inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));

@@ -1148,16 +1148,13 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
         if(uint64_t(in.m.index_offset) + 3ull * in.m.triangle_count > ctx->index_count || in.m.index_offset % 3 ||
            uint64_t(in.m.base_vertex_offset) + in.m.vertex_count > ctx->vertex_count)
             return fail(PTG_E_RANGE, "instance " + std::to_string(i) + ": mesh outside the uploaded buffers");
+        const uint32_t handle[4] = {in.blas.node_count, in.blas.node_offset, in.m.index_offset / 3, 0u};
         for(int k = 0; k < 4; ++k)
         {
-            it[i].m[k * 3 + 0] = in.inv_transform.r[k].x;
-            it[i].m[k * 3 + 1] = in.inv_transform.r[k].y;
-            it[i].m[k * 3 + 2] = in.inv_transform.r[k].z;
+            float w;
+            memcpy(&w, &handle[k], 4);
+            it[i].row[k] = make_float4(in.inv_transform.r[k].x, in.inv_transform.r[k].y, in.inv_transform.r[k].z, w);
         }
-        it[i].blas_count = in.blas.node_count;
-        it[i].blas_offset = in.blas.node_offset;
-        it[i].tri_base = in.m.index_offset / 3;
-        it[i].pad = 0;
         for(int k = 0; k < 3; ++k)
         {
             is[i].rot[k * 3 + 0] = in.transform.r[k].x;
