@@ -114,10 +114,26 @@ def main():
     ap.add_argument("--tile", type=str, default="32x16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="BASELINE.json configs[i] preset: 1 = 1280x720x256 frame 0; 2 = 1280x720x1024 frame 0 "
+                         "in pixel tiles (the metric config; tiles over the ranks); 3 = the animation at 1024 spp "
+                         "(frames/min over --animation K frames, default 30); 4 = 3840x2160x4096 frame 690 "
+                         "(dragon + buddha in view) in pixel tiles")
+    ap.add_argument("--no-frame-setup", action="store_true",
+                    help="skip the second (PCIe-inclusive, per-frame host setup) timing loop")
     ap.add_argument("--animation", type=int, default=0, metavar="K",
                     help="also render K frames spread evenly over the whole animation (frame-parallel over the "
                          "ranks) and report frames/min for the full animation (BASELINE config 4)")
     args = ap.parse_args()
+    if args.config == 1:
+        args.width, args.height, args.spp, args.frame = 1280, 720, 256, 0
+    elif args.config == 2:
+        args.width, args.height, args.spp, args.frame, args.shard = 1280, 720, 1024, 0, "tiles"
+    elif args.config == 3:
+        args.width, args.height, args.spp = 1280, 720, 1024
+        args.animation = args.animation or 30
+    elif args.config == 4:
+        args.width, args.height, args.spp, args.frame, args.shard = 3840, 2160, 4096, 690, "tiles"
 
     import numpy as np
     import torch
@@ -172,6 +188,8 @@ def main():
         r.upload(scene, include_static=False)        # per-frame TLAS/instances/subframes over PCIe
         render_step()
 
+    long_steps = cfg.width * cfg.height * cfg.samples_per_pixel > 4e9
+
     def timed(fn, timing):
         """K steps of fn between barrier + synchronize on both sides; max over ranks."""
         for _ in range(args.warmup):
@@ -182,8 +200,11 @@ def main():
         torch.cuda.synchronize(local)
         r.enable_timing(timing)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for k in range(args.steps):
             fn()    # asynchronous: host work of step k+1 overlaps the kernels of step k
+            if long_steps:   # progress for multi-minute configurations (completes step k-1 first)
+                print("step %d/%d issued at %.1f s" % (k + 1, args.steps, time.perf_counter() - t0),
+                      file=sys.stderr, flush=True)
         torch.cuda.synchronize(local)
         if world > 1:
             dist.barrier()
@@ -203,7 +224,7 @@ def main():
     step_kernel_ms = {k: v[0] for k, v in kt.items() if v[1]}
     step_kernel_n = {k: v[1] for k, v in kt.items() if v[1]}
     # (2) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
-    elapsed_frame, _ = timed(frame_step, False)
+    elapsed_frame = None if args.no_frame_setup else timed(frame_step, False)[0]
 
     anim = None
     if args.animation > 0:
@@ -242,8 +263,9 @@ def main():
 
     samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
     value = samples_per_step * args.steps / elapsed / 1e6
-    value_frame = samples_per_step * args.steps / elapsed_frame / 1e6
+    value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
 
+    is_metric = (cfg.width, cfg.height, cfg.samples_per_pixel) == (1280, 720, 1024)
     workload = "frame %d, %dx%d, %d spp, %d bounces" % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel,
                                                          cfg.max_bounces)
     result = None
@@ -297,7 +319,7 @@ def main():
                 cpu = {"value": None, "unit": "Msamples/s", "cores": None, "kind": "reference",
                        "sample": "failed: %s" % str(e)[:300]}
         result = {
-            "metric": "Msamples/sec (whole node) at 1280x720 1024spp",
+            "metric": "Msamples/sec (whole node) at %dx%d %dspp" % (cfg.width, cfg.height, cfg.samples_per_pixel),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -309,13 +331,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene assets + deterministic substitutes, frame %d" % args.frame,
-            "config": {"workload": workload + " (BASELINE metric config)",
+            "config": {"workload": workload + (" (BASELINE metric config)" if is_metric else ""),
+                       "baseline_config": args.config,
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
             "animation": anim,
-            "with_frame_setup": {"value": round(value_frame, 3), "unit": "Msamples/s",
-                                 "ms_per_step": round(elapsed_frame / args.steps * 1e3, 3),
-                                 "step": "setup_animation_frame (host) + per-frame H2D upload + render, "
-                                         "pipelined (PCIe-inclusive; not the metric)"},
+            "with_frame_setup": None if value_frame is None else {
+                "value": round(value_frame, 3), "unit": "Msamples/s",
+                "ms_per_step": round(elapsed_frame / args.steps * 1e3, 3),
+                "step": "setup_animation_frame (host) + per-frame H2D upload + render, "
+                        "pipelined (PCIe-inclusive; not the metric)"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -151,3 +151,28 @@ def test_reference_frame_0000_same_config(gpu, assets_dir):
     exact = float((own == ref).all(-1).mean())
     print("frame 0 640x360x256 vs output/frame_0000.bmp: %.2f dB, %.1f%% pixels byte-exact" % (p, 100 * exact))
     assert p >= 50.0 and exact > 0.8
+
+
+# BASELINE.json's other GPU configurations, through spot rectangles against the
+# oracle: the metric config (1024 spp, 4 sample chunks of 256) on the light
+# frame 0 and the heavy frame 450, and config 5's 3840x2160 frame with the
+# dragon and the buddha in view (frame 690; 32 spp keeps the render short -
+# the sample count changes only how many chunks the frame is cut into).
+@pytest.mark.parametrize("w,h,spp,frame,rects", [
+    (1280, 720, 1024, 0, [(0, 0, 2, 2), (640, 360, 2, 2), (1278, 718, 2, 2)]),
+    (1280, 720, 1024, 450, [(100, 80, 2, 2), (700, 400, 2, 2)]),
+    (3840, 2160, 32, 690, [(0, 0, 4, 4), (1900, 1000, 6, 4), (3000, 1500, 4, 4), (3836, 2156, 4, 4)]),
+], ids=["metric-f0", "metric-f450", "4k-f690"])
+def test_baseline_configs_spot_rects_bit_exact(gpu, assets_dir, w, h, spp, frame, rects):
+    s = scene_for(assets_dir, w, h, spp, frame=frame)
+    arr = arrays_copy(s)
+    gpu.upload_arrays(arr)
+    bgra, acc = gpu.render(s.cfg, want_accum=True)
+    gpu.synchronize()
+    bgra, acc = bgra.cpu().numpy(), acc.cpu().numpy()
+    assert bgra.shape == (h, w, 4)
+    orc = Oracle(arr, s.cfg)
+    for x0, y0, rw, rh in rects:
+        acc_o, bgra_o = orc.render_rect(x0, y0, rw, rh)
+        assert np.array_equal(_bits(acc[y0:y0 + rh, x0:x0 + rw, :3]), _bits(acc_o[..., :3])), (x0, y0)
+        assert np.array_equal(bgra[y0:y0 + rh, x0:x0 + rw], bgra_o), (x0, y0)
