@@ -41,7 +41,15 @@ struct Hit {
     bool back_face;
 };
 
-PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : 1.0f / d; }   // 1/d, 0 -> (float)1e40
+#ifndef PTG_FAST_RCP
+#define PTG_FAST_RCP 1   // the walk's reciprocals via rcp_rn (== 1.0f / x for every x, ref_math.h)
+#endif
+#if PTG_FAST_RCP
+PTG_D float wrcp(float x) { return rcp_rn(x); }
+#else
+PTG_D float wrcp(float x) { return 1.0f / x; }
+#endif
+PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : wrcp(d); }   // 1/d, 0 -> (float)1e40
 PTG_D uint32_t octant(f3 d) { return (d.x > 0 ? 1u : 0u) | (d.y > 0 ? 2u : 0u) | (d.z > 0 ? 4u : 0u); }
 
 PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
@@ -173,7 +181,12 @@ struct Walker {
             tri_base = __float_as_uint(c.w);
             inst = leaf;
             tlas_resume = node;
+#if PTG_FAST_RCP
+            bool ok = true;   // one fallback branch for the four reciprocals of the entry
+            inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
+#else
             inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+#endif
             base = boffset * 8 + octant(bd) * bcount;
             count = bcount;
             node = 0;
@@ -183,7 +196,16 @@ struct Walker {
             axis = 2;
             if(ax > ay && ax > az) { axis = 0; rd = V3(bd.z, bd.y, bd.x); }
             else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
+#if PTG_FAST_RCP
+            float k = rcp_nr(rd.z, ok);
+            if(!ok)
+            {   // a zero, denormal or huge component (rare): IEEE division
+                inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+                k = 1.0f / rd.z;
+            }
+#else
             const float k = 1.0f / rd.z;
+#endif
             S = V3(rd.x * k, rd.y * k, 1.0f * k);
             return 0;
         }
@@ -204,7 +226,7 @@ struct Walker {
         if(!(det != 0.0f && ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
                              (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f))))
             return 0;
-        const float rdet = 1.0f / det;
+        const float rdet = wrcp(det);
         const float u = uvw.x * rdet, v = uvw.y * rdet, t = dot(uvw, S.z * z) * rdet;
         bool back = det < 0;
         if(S.z < 0) back = !back;

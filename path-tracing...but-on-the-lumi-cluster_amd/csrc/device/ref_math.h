@@ -43,6 +43,29 @@ PTG_D f3 operator-(f3 a) { return V3(-a.x, -a.y, -a.z); }
 PTG_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PTG_D f3 cross(f3 a, f3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 
+// 1.0f / x, correctly rounded, without the full IEEE division sequence
+// (v_div_scale / v_div_fmas / v_div_fixup and the denormal-mode switches):
+// the hardware reciprocal (about 1 ulp) plus one Newton step with FMA gives the
+// correctly rounded reciprocal for every x whose reciprocal is a normal
+// number; the rest (zeros, denormals, |x| >= 2^126, inf, NaN) take the
+// division.  tools/rcp_exhaustive.hip checks all 2^32 inputs against 1.0f / x
+// on the GPU, bit for bit.
+// rcp_nr(x, ok): the fast path alone; ok is cleared when x is outside its
+// range, and the caller then takes the division (one branch for several).
+PTG_D float rcp_nr(float x, bool& ok)
+{
+    ok = ok && ((__float_as_uint(x) >> 23) & 0xFFu) - 1u < 252u;
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float err = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(err, r, r);
+}
+PTG_D float rcp_rn(float x)
+{
+    bool ok = true;
+    const float r = rcp_nr(x, ok);
+    return ok ? r : 1.0f / x;
+}
+
 // f32 sqrt: correctly rounded == the reference's (float)sqrt((double)x)
 PTG_D float fsqrt(float x) { return __builtin_sqrtf(x); }
 PTG_D float length(f3 a) { return fsqrt(dot(a, a)); }
