@@ -59,6 +59,96 @@ PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
     hi = q[1];
 }
 
+// Where a walk keeps its cold state - the world ray, its reciprocal, the
+// TLAS resume point and the best hit so far.  They are touched only when a
+// BLAS is entered or left and when a hit is confirmed, so a walker can keep
+// them in registers (RegCold) or, where registers decide the occupancy, in a
+// per-lane LDS slot (LdsCold, the wavefront walk kernels).
+struct RegCold {
+    f3 o, d, inv_w;            // world ray and its reciprocal direction
+    uint32_t tlas_base, tlas_count, tlas_resume;
+    Hit best;
+
+    PTG_D void init(f3 ro, f3 rd, f3 iw, uint32_t tb, uint32_t tc)
+    {
+        o = ro; d = rd; inv_w = iw;
+        tlas_base = tb; tlas_count = tc; tlas_resume = 0;
+        best.thit = -1.0f;
+        best.bx = best.by = best.bz = 0.0f;
+        best.instance_id = 0xFFFFFFFFu;
+        best.primitive_id = 0;
+        best.back_face = false;
+    }
+    PTG_D f3 world_o() const { return o; }
+    PTG_D f3 world_d() const { return d; }
+    PTG_D void leave_blas(f3& org, f3& inv, uint32_t& base, uint32_t& node, uint32_t& count) const
+    {
+        base = tlas_base; org = o; inv = inv_w; node = tlas_resume; count = tlas_count;
+    }
+    PTG_D void set_resume(uint32_t n) { tlas_resume = n; }
+    // ray_query_confirm (ray_query.hh:280-290)
+    PTG_D void confirm(float u, float v, float t, uint32_t instance, uint32_t prim, bool back)
+    {
+        best.bx = u;
+        best.by = v;
+        best.bz = 1.0f - u - v;
+        best.thit = t;
+        best.instance_id = instance;
+        best.primitive_id = prim;
+        best.back_face = back;
+    }
+    PTG_D Hit result(float) const { return best; }
+};
+
+struct WalkCold {              // one lane's LDS slot: four conflict-free b128 accesses
+    float4 o;                  // world origin xyz, TLAS record base
+    float4 d;                  // world direction xyz, TLAS node count
+    float4 inv;                // 1/direction xyz, TLAS node to resume after the BLAS
+    float4 best;               // closest hit so far: u, v, instance, primitive | back_face << 31
+};
+
+struct LdsCold {
+    WalkCold* c;
+
+    PTG_D void init(f3 ro, f3 rd, f3 iw, uint32_t tb, uint32_t tc)
+    {
+        c->o = make_float4(ro.x, ro.y, ro.z, __uint_as_float(tb));
+        c->d = make_float4(rd.x, rd.y, rd.z, __uint_as_float(tc));
+        c->inv = make_float4(iw.x, iw.y, iw.z, __uint_as_float(0u));
+        c->best = make_float4(0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu), __uint_as_float(0u));
+    }
+    PTG_D f3 world_o() const { const float4 v = c->o; return V3(v.x, v.y, v.z); }
+    PTG_D f3 world_d() const { const float4 v = c->d; return V3(v.x, v.y, v.z); }
+    PTG_D void leave_blas(f3& org, f3& inv, uint32_t& base, uint32_t& node, uint32_t& count) const
+    {
+        const float4 wo = c->o, wd = c->d, wi = c->inv;
+        base = __float_as_uint(wo.w); org = V3(wo.x, wo.y, wo.z);
+        inv = V3(wi.x, wi.y, wi.z); node = __float_as_uint(wi.w); count = __float_as_uint(wd.w);
+    }
+    PTG_D void set_resume(uint32_t n) { c->inv.w = __uint_as_float(n); }
+    // ray_query_confirm (ray_query.hh:280-290); thit is the walk's tmax, bz is
+    // derived in result() with the same arithmetic
+    PTG_D void confirm(float u, float v, float, uint32_t instance, uint32_t prim, bool back)
+    {
+        c->best = make_float4(u, v, __uint_as_float(instance), __uint_as_float(prim | (back ? 0x80000000u : 0u)));
+    }
+    PTG_D Hit result(float tmax) const
+    {
+        const float4 b = c->best;
+        const uint32_t id = __float_as_uint(b.z), pb = __float_as_uint(b.w);
+        const bool hit = id != 0xFFFFFFFFu;
+        Hit h;
+        h.bx = b.x;
+        h.by = b.y;
+        h.bz = hit ? 1.0f - b.x - b.y : 0.0f;
+        h.thit = hit ? tmax : -1.0f;
+        h.instance_id = id;
+        h.primitive_id = pb & 0x7FFFFFFFu;
+        h.back_face = (pb >> 31) != 0;
+        return h;
+    }
+};
+
 // One ray query, resumable: the walk state of ray_query (ray_query.hh:66-109)
 // for both levels, advanced one BVH step at a time by step().  ANY = true is
 // trace_shadow_ray (path_tracer.hh:415-427): the first accepted candidate
@@ -67,43 +157,33 @@ PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
 // shortens tmax.  The flat step (TLAS node, BLAS node, BLAS entry, triangle
 // test or BLAS exit) keeps the lanes of a wave stepping together whatever
 // level each one is in.
-struct Walker {
-    f3 o, d, inv_w;            // world ray and its reciprocal direction
+template<class Cold>
+struct WalkerT {
+    Cold cold;                 // world ray, TLAS resume point, best hit
     float tmin, tmax;
-    uint32_t tlas_base, tlas_count;
     f3 org, inv;               // active level: ray origin / 1/dir in that level's space
     uint32_t base, node, count;
-    uint32_t tlas_resume;      // TLAS node to continue with after the BLAS
     f3 S;                      // BLAS: shear constants of ray_triangle_intersection_preprocess
     int axis;                  // BLAS: dominant axis, -1 while in the TLAS (blas_axis)
     uint32_t tri_base, inst;
-    Hit best;
 
     PTG_D void init(const DevScene& sc, uint32_t tc, uint32_t to, f3 ro, f3 rd, float t0, float t1)
     {
-        o = ro;
-        d = rd;
-        inv_w = V3(rcp_or_big(rd.x), rcp_or_big(rd.y), rcp_or_big(rd.z));
+        const f3 iw = V3(rcp_or_big(rd.x), rcp_or_big(rd.y), rcp_or_big(rd.z));
+        base = to * 8 + octant(rd) * tc;
+        cold.init(ro, rd, iw, base, tc);
         tmin = t0;
         tmax = t1;
-        tlas_count = tc;
-        tlas_base = to * 8 + octant(rd) * tc;
-        org = o;
-        inv = inv_w;
-        base = tlas_base;
+        org = ro;
+        inv = iw;
         node = 0;
         count = tc;
-        tlas_resume = 0;
         S = V3(0, 0, 0);
         axis = -1;
         tri_base = 0;
         inst = 0xFFFFFFFFu;
-        best.thit = -1.0f;
-        best.bx = best.by = best.bz = 0.0f;
-        best.instance_id = 0xFFFFFFFFu;
-        best.primitive_id = 0;
-        best.back_face = false;
     }
+    PTG_D Hit result() const { return cold.result(tmax); }
 
     // slab test (ray_query.hh:197-207); min/max results only feed compares
     PTG_D bool box_hit(float4 lo, float4 hi) const
@@ -126,11 +206,7 @@ struct Walker {
             if(axis < 0) return 1;
             // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
             axis = -1;
-            base = tlas_base;
-            org = o;
-            inv = inv_w;
-            node = tlas_resume;
-            count = tlas_count;
+            cold.leave_blas(org, inv, base, node, count);
             return 0;
         }
         float4 lo, hi;
@@ -171,6 +247,7 @@ struct Walker {
             const v4f a = ip[0], b = ip[1], c = ip[2], e = ip[3];
             // rows M0..M3 of inv_transform in xyz; w: blas count, offset, tri_base
             const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(b.x, b.y, b.z), M2 = V3(c.x, c.y, c.z), M3 = V3(e.x, e.y, e.z);
+            const f3 o = cold.world_o(), d = cold.world_d();
             org = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
                      M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
                      M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
@@ -180,7 +257,7 @@ struct Walker {
             const uint32_t bcount = __float_as_uint(a.w), boffset = __float_as_uint(b.w);
             tri_base = __float_as_uint(c.w);
             inst = leaf;
-            tlas_resume = node;
+            cold.set_resume(node);
 #if PTG_FAST_RCP
             bool ok = true;   // one fallback branch for the four reciprocals of the entry
             inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
@@ -234,19 +311,14 @@ struct Walker {
         if(t >= 0.0f && t < tmax && t > tmin)
         {
             if(ANY) return 2;
-            // ray_query_confirm (ray_query.hh:280-290)
-            best.bx = u;
-            best.by = v;
-            best.bz = 1.0f - u - v;
-            best.thit = t;
-            best.instance_id = inst;
-            best.primitive_id = leaf;
-            best.back_face = back;
+            cold.confirm(u, v, t, inst, leaf, back);
             tmax = t;
         }
         return 0;
     }
 };
+
+using Walker = WalkerT<RegCold>;
 
 // A whole query on one lane.  Returns whether the ray hit (ANY: occluded).
 template<bool ANY, bool COUNT>
@@ -258,7 +330,7 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
     w.init(sc, tlas_count, tlas_offset, o, d, tmin, tmax);
     int r;
     while((r = w.template step<ANY, COUNT>(sc, cnt)) == 0) {}
-    best = w.best;
+    best = w.result();
     return ANY ? r == 2 : best.thit >= 0.0f;
 }
 

@@ -252,6 +252,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WALK_UNROLL
 #define PTG_WALK_UNROLL 2   // walk steps per refill check (measured: 2 beats 1 and 3)
 #endif
+#ifndef PTG_WALK_LDS
+#define PTG_WALK_LDS 1
+#endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
 #endif
@@ -281,7 +284,15 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
+#if PTG_WALK_LDS
+    // the walk's cold state in LDS: 64 VGPRs instead of 76, so a sky wave
+    // fits beside six walk waves on a SIMD (see ptg_context_create)
+    extern __shared__ WalkCold cold[];
+    WalkerT<LdsCold> w;
+    w.cold.c = &cold[threadIdx.x];
+#else
     Walker w;
+#endif
     bool active = false;
     uint32_t q = 0;
     for(;;)
@@ -321,7 +332,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                 if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
                 else
                 {
-                    const Hit& h = w.best;
+                    const Hit h = w.result();
                     tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
                     tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
                 }
@@ -663,7 +674,8 @@ struct ptg_context {
     int pipeline = 0;
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
-    uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
+    uint32_t walk_xcds[2] = {1, 1};
+    uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state, padded to cap residency        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t chunk_log2 = 28;              // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2)   // resident blocks of k_wf_walk<closest/any>
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
@@ -850,10 +862,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 const TraceOut& tr = trs[r & 1];
                 if(int e = timed_begin(ctx, K_EXTEND)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ctx->stream, sc, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
                 else
-                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), 0, ctx->stream, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ctx->stream, sc, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx)) return e;
@@ -864,10 +876,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 {
                     if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
                     if(ctx->counting)
-                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), 0, ss, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
                     else
-                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), 0, ss, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
                     PTG_HIP(hipGetLastError());
                     if(int e = timed_end(ctx, ss)) return e;
@@ -1030,10 +1042,24 @@ int ptg_context_create(int device, ptg_context** out)
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * per_cu_blocks;
     // walk grids: a multiple of what is resident at once (the queue is split
     // statically over the waves of the whole grid)
+#if PTG_WALK_LDS
+    // Walk residency: the walks' VGPRs (64) allow 8 blocks/CU, but at 8 the
+    // sky and shade kernels on the other stream cannot get a wave onto a
+    // SIMD until walk waves retire.  The walk blocks' LDS (cold state padded)
+    // sets how many are resident: 6 (default) leaves 128 VGPRs per SIMD free.
+    uint32_t resident[2] = {6, 6};
+    if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
+    if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
+    const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
+    for(int k = 0; k < 2; ++k)
+        ctx->walk_lds[k] = std::max<uint32_t>(kBlock * sizeof(WalkCold), (lds_cu / resident[k]) / 1024u * 1024u);
+#endif
     int per_cu = 0;
-    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, 0) == hipSuccess && per_cu > 0)
+    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, ctx->walk_lds[0]) == hipSuccess &&
+       per_cu > 0)
         ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
-    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, 0) == hipSuccess && per_cu > 0)
+    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, ctx->walk_lds[1]) == hipSuccess &&
+       per_cu > 0)
         ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
     // 4 x the resident grid: each block's static share is a quarter, and the
     // dispatcher starts the later blocks as earlier ones retire, which trims
