@@ -676,6 +676,7 @@ struct ptg_context {
     uint32_t walk_grid[2] = {2048, 2048};
     uint32_t walk_xcds[2] = {1, 1};
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state, padded to cap residency        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
+    uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM (PTG_HBM_PCT)
     uint32_t chunk_log2 = 28;              // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2)   // resident blocks of k_wf_walk<closest/any>
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
@@ -767,7 +768,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
         const size_t per_path = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 4 * 4 + sizeof(float4);
-        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * 35 / per_path));
+        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * ctx->hbm_pct / per_path));
     }
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
     const uint32_t span = j1 - j0;
@@ -1036,7 +1037,8 @@ int ptg_context_create(int device, ptg_context** out)
     ctx->counting = cnt && cnt[0] == '1';
     const char* pipe = getenv("PTG_PIPELINE");
     if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
-    if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(28, std::max(16, atoi(c))));
+    if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(30, std::max(16, atoi(c))));
+    if(const char* c = getenv("PTG_HBM_PCT")) ctx->hbm_pct = uint32_t(std::min(70, std::max(5, atoi(c))));
     uint32_t per_cu_blocks = 32;   // grid-stride kernels (camera, shade): measured best of 3..128
     if(const char* w = getenv("PTG_BLOCKS_PER_CU")) per_cu_blocks = uint32_t(std::max(1, atoi(w)));
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * per_cu_blocks;
