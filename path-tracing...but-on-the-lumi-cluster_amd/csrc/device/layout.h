@@ -74,9 +74,14 @@ struct DevScene {
     const float* albedo;           // float4[]
     const float* material;         // float4[]
     const uint8_t* subframes;      // reference subframe[] (160 B each)
+    const float2* polygon;         // per subframe: (sin, cos) of the aperture polygon's vertex angles (kPolyStride each)
     uint32_t width, height, spp, max_bounces, student_id, blur_step;
     uint32_t subframe_count;
 };
+
+// Aperture polygons with at most kPolyMaxSides sides read their vertex
+// directions from DevScene::polygon (k_polygon_table).
+constexpr uint32_t kPolyMaxSides = 30, kPolyStride = kPolyMaxSides + 2;
 
 // Reference subframe byte offsets (scene.hh:26-34, verified in include/ptg.h users)
 enum : uint32_t {

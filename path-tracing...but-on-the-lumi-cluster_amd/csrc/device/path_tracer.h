@@ -448,15 +448,33 @@ PTG_D f3 sample_cone(f3 dir, float cos_min, f2 u)                      // :40-48
     const float phi = u.y * 2.0f * PI_F;
     return mul_m3v3(tangent_space(dir), V3(fcos(phi) * st, fsin(phi) * st, ct));
 }
-PTG_D f2 regular_polygon(f2 u, float angle, uint32_t sides)            // :50-62
+// Vertex k of the aperture polygon: angle side_radians * k + angle, as
+// regular_polygon forms it for k = side and k = side + 1 (side + 1.0f is the
+// float k exactly); (sin, cos) in double, rounded to float.
+PTG_D f2 polygon_vertex(float angle, uint32_t sides, float k)
+{
+    const float side_radians = (2.0f * PI_F) / (float)sides;
+    const float a = side_radians * k + angle;
+    return f2{fsin(a), fcos(a)};
+}
+// table: the polygon_vertex values of this subframe (k = 0 .. sides + 1), or null
+PTG_D f2 regular_polygon(f2 u, float angle, uint32_t sides, const float2* table = nullptr)   // :50-62
 {
     const float side = (float)floor((double)(u.x * (float)sides));
     u.x *= (float)sides;
     u.x = (float)((double)u.x - floor((double)u.x));
-    const float side_radians = (2.0f * PI_F) / (float)sides;
-    const float a1 = side_radians * side + angle;
-    const float a2 = side_radians * (side + 1.0f) + angle;
-    const f2 b{fsin(a1), fcos(a1)}, c{fsin(a2), fcos(a2)};
+    f2 b, c;
+    if(table)
+    {   // side is an integer in [0, sides] (u.x may round to 1.0)
+        const float2 tb = table[(uint32_t)side], tc = table[(uint32_t)side + 1u];
+        b = f2{tb.x, tb.y};
+        c = f2{tc.x, tc.y};
+    }
+    else
+    {
+        b = polygon_vertex(angle, sides, side);
+        c = polygon_vertex(angle, sides, side + 1.0f);
+    }
     if(u.x + u.y > 1.0f) { u.x = 1.0f - u.x; u.y = 1.0f - u.y; }
     return f2{b.x * u.x + c.x * u.y, b.y * u.x + c.y * u.y};
 }
@@ -807,7 +825,10 @@ PTG_D void camera_ray(const DevScene& sc, const uint8_t* sf, uint32_t px, uint32
     const int32_t polygon = (int32_t)rd_u(cam, 80);
     if(polygon > 3)
     {
-        const f2 p = regular_polygon(f2{u.z, u.w}, rd_f(cam, 76), (uint32_t)polygon);
+        const uint32_t sub = (uint32_t)(sf - sc.subframes) / SF_STRIDE;
+        const float2* table = (sc.polygon && (uint32_t)polygon <= kPolyMaxSides) ? sc.polygon + size_t(sub) * kPolyStride
+                                                                                 : nullptr;
+        const f2 p = regular_polygon(f2{u.z, u.w}, rd_f(cam, 76), (uint32_t)polygon, table);
         const float rad = rd_f(cam, 84);
         ap = f2{p.x * rad, p.y * rad};
     }

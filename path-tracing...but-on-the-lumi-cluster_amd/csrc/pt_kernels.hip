@@ -115,6 +115,24 @@ __global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh
     }
 }
 
+// The aperture polygon's vertex directions of every subframe (regular_polygon,
+// path_tracer.hh:50-62): (sin, cos) of side_radians * k + angle for
+// k = 0 .. sides + 1.  A polygon has few vertices and every sample's camera
+// ray uses two of them, so the camera kernel reads them instead of making
+// four double-precision trig calls.  One thread per (subframe, k).
+__global__ void k_polygon_table(const uint8_t* __restrict__ subframes, uint32_t count, float2* __restrict__ out)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if(t >= count * kPolyStride) return;
+    const uint32_t i = t / kPolyStride, k = t % kPolyStride;
+    const uint8_t* cam = subframes + size_t(i) * SF_STRIDE + SF_CAM;
+    const int32_t sides = (int32_t)rd_u(cam, 80);
+    f2 v{0.0f, 0.0f};
+    if(sides > 3 && (uint32_t)sides <= kPolyMaxSides && k <= (uint32_t)sides + 1u)
+        v = polygon_vertex(rd_f(cam, 76), (uint32_t)sides, (float)k);
+    out[t] = make_float2(v.x, v.y);
+}
+
 struct MeshJob {
     uint32_t index_offset, triangle_count, base_vertex_offset, pad;
 };
@@ -658,7 +676,7 @@ struct ptg_context {
     std::unordered_set<uint32_t> packed_bvh, packed_mesh;
     bool scene_ready = false;
     // frame
-    DevBuf frame_nodes, frame_links, subframes, inst_trav, inst_shade, jobs;
+    DevBuf frame_nodes, frame_links, subframes, inst_trav, inst_shade, jobs, polygon;
     size_t first_frame_node = 0, frame_node_count = 0, subframe_count = 0, instance_count = 0;
     std::vector<ptg_subframe> host_subframes;
     bool frame_ready = false;
@@ -704,6 +722,7 @@ struct ptg_context {
         s.albedo = albedo.as<float>();
         s.material = material.as<float>();
         s.subframes = subframes.as<uint8_t>();
+        s.polygon = polygon.as<float2>();
         s.width = cfg ? cfg->width : 0;
         s.height = cfg ? cfg->height : 0;
         s.spp = cfg ? cfg->samples_per_pixel : 0;
@@ -1224,6 +1243,10 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
     PTG_HIP(hipMemcpyAsync(ctx->inst_trav.p, it.data(), instance_count * sizeof(InstTrav), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->inst_shade.p, is.data(), instance_count * sizeof(InstShade), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->subframes.p, subframes, subframe_count * sizeof(ptg_subframe), hipMemcpyHostToDevice, s));
+    PTG_HIP(ctx->polygon.reserve(subframe_count * kPolyStride * sizeof(float2)));
+    hipLaunchKernelGGL(k_polygon_table, dim3(grid_for(subframe_count * kPolyStride)), dim3(kBlock), 0, s,
+                       ctx->subframes.as<uint8_t>(), uint32_t(subframe_count), ctx->polygon.as<float2>());
+    PTG_HIP(hipGetLastError());
     PTG_HIP(hipMemcpyAsync(ctx->frame_nodes.p, frame_nodes, frame_node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->frame_links.p, frame_links, 8 * frame_node_count * sizeof(ptg_bvh_link),
                            hipMemcpyHostToDevice, s));
