@@ -273,6 +273,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WALK_LDS
 #define PTG_WALK_LDS 1
 #endif
+#ifndef PTG_WF_SLOTS
+#define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
+#endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
 #endif
@@ -701,11 +704,32 @@ struct ptg_context {
     // second stream for the sky kernels + the events that order it with `stream`
     hipStream_t side = nullptr;
     hipEvent_t ev_main = nullptr, ev_side = nullptr;
+    // Wavefront chunk pipelines ("slots").  With two slots, consecutive
+    // chunks run concurrently on their own stream pairs and buffers, so one
+    // chunk's round-0 walk and shade overlap the other's sky and shadow
+    // kernels; k_accumulate still folds the chunks in sample order, on
+    // acc_stream.  Slot 0 is the context's own stream pair and buffers.
+    struct Slot {
+        hipStream_t main = nullptr, side = nullptr;
+        hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_done = nullptr, ev_acc = nullptr;
+        DevBuf own_state, own_samples;
+        DevBuf* state = nullptr;
+        DevBuf* samples = nullptr;
+    };
+    Slot slot[2];
+    uint32_t nslots = 1;
+    hipStream_t acc_stream = nullptr;
+    hipEvent_t ev_render_start = nullptr, ev_acc_end = nullptr;
     ~ptg_context()
     {
         if(ev_main) (void)hipEventDestroy(ev_main);
         if(ev_side) (void)hipEventDestroy(ev_side);
         if(side) (void)hipStreamDestroy(side);
+        Slot& b = slot[1];
+        for(hipEvent_t e: {b.ev_main, b.ev_side, b.ev_done, b.ev_acc, slot[0].ev_done, slot[0].ev_acc, ev_render_start, ev_acc_end})
+            if(e) (void)hipEventDestroy(e);
+        for(hipStream_t st: {b.main, b.side, acc_stream})
+            if(st) (void)hipStreamDestroy(st);
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
         for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
     }
@@ -781,6 +805,17 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     // Wavefront chunks are as large as HBM allows (capped at 35% of it): every
     // bounce round then launches over a long queue, so the walk and shade
     // launches run at full occupancy with short tails.  2^28 paths = 93 GB.
+    // wavefront chunk pipelines: slot 0 is the context's stream pair and buffers
+    const uint32_t nslots = wf ? ctx->nslots : 1u;
+    ptg_context::Slot* slots = ctx->slot;
+    slots[0].main = ctx->stream;
+    slots[0].side = ctx->side;
+    slots[0].ev_main = ctx->ev_main;
+    slots[0].ev_side = ctx->ev_side;
+    slots[0].state = &ctx->wf_state;
+    slots[0].samples = &ctx->samples;
+    slots[1].state = &slots[1].own_state;
+    slots[1].samples = &slots[1].own_samples;
     size_t target = (size_t(1) << 30) / sizeof(float4);
     if(wf)
     {
@@ -792,11 +827,14 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
     const uint32_t span = j1 - j0;
     const uint32_t max_chunk = std::max<uint32_t>(8, uint32_t(std::min<size_t>(target / size_t(pm.npix), span)) & ~7u);
-    const uint32_t nchunks = (span + max_chunk - 1) / max_chunk;
+    uint32_t nchunks = (span + max_chunk - 1) / max_chunk;
+    if(nslots > 1 && span >= 16u)
+        nchunks = (std::max(nchunks, nslots) + nslots - 1) / nslots * nslots;   // whole rounds over the slots
     uint32_t chunk = std::min<uint32_t>(span, ((span + nchunks - 1) / nchunks + 7) & ~7u);
     const size_t M = size_t((pm.npix + 7) / 8) * ((chunk + 7) / 8) * 64;   // lanes per chunk (upper bound)
     if(M >= (1ull << 31)) return fail(PTG_E_RANGE, "chunk too large");
-    PTG_HIP(ctx->samples.reserve(size_t(pm.npix) * chunk * sizeof(float4)));
+    for(uint32_t k = 0; k < nslots; ++k)
+        PTG_HIP(slots[k].samples->reserve(size_t(pm.npix) * chunk * sizeof(float4)));
     PTG_HIP(ctx->acc.reserve(size_t(pm.npix) * sizeof(float4)));
     unsigned long long* cnt_dev = nullptr;
     if(ctx->counting)
@@ -806,92 +844,114 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         cnt_dev = ctx->counters.as<unsigned long long>();
     }
     const uint32_t rounds = cfg->max_bounces + 1;
-    PathSoA S[2];
-    TraceOut trs[2] = {};   // per round parity: the sky kernel of round r reads its set while round r+1 writes the other
-    uint32_t* lists[2] = {nullptr, nullptr};
-    uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
-    uint32_t* counts = nullptr;
+    // path state of a slot: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
+    struct SlotState {
+        PathSoA S[2];
+        TraceOut trs[2] = {};   // per round parity: the sky kernel of round r reads its set while round r+1 writes the other
+        uint32_t* lists[2] = {nullptr, nullptr};
+        uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
+        uint32_t* counts = nullptr;
+    } st[2];
     if(wf)
-    {
-        // path state: 2 x 9 records of 16 B per path, + trace outputs + NEE lists
-        const size_t rec = M * 16;
-        PTG_HIP(ctx->wf_state.reserve(2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
-        char* b = ctx->wf_state.as<char>();
-        for(int h = 0; h < 2; ++h)
+        for(uint32_t k = 0; k < nslots; ++k)
         {
-            S[h].meta = reinterpret_cast<uint4*>(b); b += rec;
-            S[h].seed = reinterpret_cast<uint4*>(b); b += rec;
-            S[h].ray_o = reinterpret_cast<float4*>(b); b += rec;
-            S[h].ray_d = reinterpret_cast<float4*>(b); b += rec;
-            S[h].att = reinterpret_cast<float4*>(b); b += rec;
-            S[h].contrib = reinterpret_cast<float4*>(b); b += rec;
-            S[h].batt = reinterpret_cast<float4*>(b); b += rec;
-            S[h].nee_c = reinterpret_cast<float4*>(b); b += rec;
-            S[h].nee_d = reinterpret_cast<float4*>(b); b += rec;
+            const size_t rec = M * 16;
+            PTG_HIP(slots[k].state->reserve(2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+            char* b = slots[k].state->as<char>();
+            SlotState& t = st[k];
+            for(int h = 0; h < 2; ++h)
+            {
+                t.S[h].meta = reinterpret_cast<uint4*>(b); b += rec;
+                t.S[h].seed = reinterpret_cast<uint4*>(b); b += rec;
+                t.S[h].ray_o = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].ray_d = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].att = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].contrib = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].batt = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].nee_c = reinterpret_cast<float4*>(b); b += rec;
+                t.S[h].nee_d = reinterpret_cast<float4*>(b); b += rec;
+            }
+            for(TraceOut& o: t.trs)
+            {
+                o.hit = reinterpret_cast<uint4*>(b); b += M * 16;
+                o.bary = reinterpret_cast<float4*>(b); b += M * 16;
+                o.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            }
+            t.lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.sky_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.counts = reinterpret_cast<uint32_t*>(b);
         }
-        for(TraceOut& t: trs)
-        {
-            t.hit = reinterpret_cast<uint4*>(b); b += M * 16;
-            t.bary = reinterpret_cast<float4*>(b); b += M * 16;
-            t.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
-        }
-        lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
-        lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
-        hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
-        sky_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
-        counts = reinterpret_cast<uint32_t*>(b);
+    if(nslots > 1)
+    {   // the other slot and the accumulation stream start after what the caller queued
+        PTG_HIP(hipEventRecord(ctx->ev_render_start, ctx->stream));
+        PTG_HIP(hipStreamWaitEvent(slots[1].main, ctx->ev_render_start, 0));
+        PTG_HIP(hipStreamWaitEvent(ctx->acc_stream, ctx->ev_render_start, 0));
     }
     const DevScene sc = ctx->scene_args(cfg);
     const uint32_t persistent = ctx->persistent_blocks;
     const bool overlap = wf && ctx->side != nullptr;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
-    for(uint32_t j = j0; j < j1; j += chunk)
+    uint32_t chunk_index = 0;
+    for(uint32_t j = j0; j < j1; j += chunk, ++chunk_index)
     {
         const uint32_t nj = std::min(chunk, j1 - j);
+        ptg_context::Slot& sl = slots[chunk_index % nslots];
+        SlotState& sst = st[chunk_index % nslots];
+        PathSoA* S = sst.S;
+        TraceOut* trs = sst.trs;
+        uint32_t** lists = sst.lists;
+        uint32_t* hit_list = sst.hit_list;
+        uint32_t* sky_list = sst.sky_list;
+        uint32_t* counts = sst.counts;
+        const hipStream_t ms = sl.main;
+        if(nslots > 1 && chunk_index >= nslots)
+            PTG_HIP(hipStreamWaitEvent(ms, sl.ev_acc, 0));   // its samples buffer was folded in
         const size_t lanes = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8) * 64;
-        float4* out = ctx->samples.as<float4>();
+        float4* out = sl.samples->as<float4>();
         if(!wf)
         {
-            if(int r = timed_begin(ctx, K_MEGA)) return r;
+            if(int r = timed_begin(ctx, K_MEGA, ms)) return r;
             if(ctx->counting)
-                hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(lanes)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, out,
+                hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(lanes)), dim3(kBlock), 0, ms, sc, pm, j, nj, out,
                                    cnt_for(K_MEGA));
             else
-                hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(lanes)), dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, out,
+                hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(lanes)), dim3(kBlock), 0, ms, sc, pm, j, nj, out,
                                    nullptr);
             PTG_HIP(hipGetLastError());
-            if(int r = timed_end(ctx)) return r;
+            if(int r = timed_end(ctx, ms)) return r;
         }
         else
         {
-            PTG_HIP(hipMemsetAsync(counts, 0, 4 * (rounds + 2) * sizeof(uint32_t), ctx->stream));
+            PTG_HIP(hipMemsetAsync(counts, 0, 4 * (rounds + 2) * sizeof(uint32_t), ms));
             const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(persistent, grid_for(lanes))));
-            if(int r = timed_begin(ctx, K_CAMERA)) return r;
+            if(int r = timed_begin(ctx, K_CAMERA, ms)) return r;
             if(ctx->counting)
-                hipLaunchKernelGGL(k_wf_camera<true>, grid, dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, uint32_t(lanes),
+                hipLaunchKernelGGL(k_wf_camera<true>, grid, dim3(kBlock), 0, ms, sc, pm, j, nj, uint32_t(lanes),
                                    S[0], counts, out, cnt_for(K_CAMERA));
             else
-                hipLaunchKernelGGL(k_wf_camera<false>, grid, dim3(kBlock), 0, ctx->stream, sc, pm, j, nj, uint32_t(lanes),
+                hipLaunchKernelGGL(k_wf_camera<false>, grid, dim3(kBlock), 0, ms, sc, pm, j, nj, uint32_t(lanes),
                                    S[0], counts, out, nullptr);
             PTG_HIP(hipGetLastError());
-            if(int r = timed_end(ctx)) return r;
+            if(int r = timed_end(ctx, ms)) return r;
             for(uint32_t r = 0; r < rounds; ++r)
             {
                 const PathSoA& cur = S[r & 1];
                 const PathSoA& nxt = S[(r + 1) & 1];
                 const TraceOut& tr = trs[r & 1];
-                if(int e = timed_begin(ctx, K_EXTEND)) return e;
+                if(int e = timed_begin(ctx, K_EXTEND, ms)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ctx->stream, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
                 else
-                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ctx->stream, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
-                if(int e = timed_end(ctx)) return e;
+                if(int e = timed_end(ctx, ms)) return e;
                 // second stream: the previous round's sky kernel, then this round's
                 // shadow walk (independent of the closest-hit walk it runs beside)
-                hipStream_t ss = overlap ? ctx->side : ctx->stream;
+                hipStream_t ss = overlap ? sl.side : ms;
                 if(r > 0)
                 {
                     if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
@@ -909,30 +969,30 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 // kernel read, and the state set it read
                 if(overlap)
                 {
-                    PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
-                    PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
+                    PTG_HIP(hipEventRecord(sl.ev_side, sl.side));
+                    PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
                 }
-                if(int e = timed_begin(ctx, K_CLASSIFY)) return e;
-                hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ctx->stream, counts, r, tr, cur.meta, hit_list,
+                if(int e = timed_begin(ctx, K_CLASSIFY, ms)) return e;
+                hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ms, counts, r, tr, cur.meta, hit_list,
                                    sky_list, lc);
                 PTG_HIP(hipGetLastError());
-                if(int e = timed_end(ctx)) return e;
-                if(int e = timed_begin(ctx, K_SHADE)) return e;
+                if(int e = timed_end(ctx, ms)) return e;
+                if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
+                    hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
                                        hit_list, lc, lists[(r + 1) & 1], out, cnt_for(K_SHADE));
                 else
-                    hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ctx->stream, sc, cur, nxt, counts, r, tr,
+                    hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
                                        hit_list, lc, lists[(r + 1) & 1], out, nullptr);
                 PTG_HIP(hipGetLastError());
-                if(int e = timed_end(ctx)) return e;
+                if(int e = timed_end(ctx, ms)) return e;
                 // escaped rays retire without feeding the next round: their
                 // double-precision atmosphere runs on the second stream, overlapping
                 // the next round's latency-bound walks
                 if(overlap)
                 {
-                    PTG_HIP(hipEventRecord(ctx->ev_main, ctx->stream));
-                    PTG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+                    PTG_HIP(hipEventRecord(sl.ev_main, ms));
+                    PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
@@ -945,26 +1005,40 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             }
             if(overlap)
             {   // join before accumulate
-                PTG_HIP(hipEventRecord(ctx->ev_side, ctx->side));
-                PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0));
+                PTG_HIP(hipEventRecord(sl.ev_side, sl.side));
+                PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
             }
         }
         if(wf && getenv("PTG_DEBUG_QUEUES"))
         {   // diagnostics: per-round queue sizes of this chunk
             std::vector<uint32_t> h(2 * (rounds + 2));
-            PTG_HIP(hipMemcpyAsync(h.data(), counts, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-            PTG_HIP(hipStreamSynchronize(ctx->stream));
+            PTG_HIP(hipMemcpyAsync(h.data(), counts, h.size() * 4, hipMemcpyDeviceToHost, ms));
+            PTG_HIP(hipStreamSynchronize(ms));
             fprintf(stderr, "chunk j=%u nj=%u lanes=%zu counts:", j, nj, lanes);
             for(uint32_t v: h) fprintf(stderr, " %u", v);
             fprintf(stderr, "\n");
         }
+        // fold the chunk into the running per-pixel sums, chunks in sample order
         const int first = j == j0, last = j + nj >= j1;
-        if(int r = timed_begin(ctx, K_ACCUM)) return r;
-        hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, ctx->stream, pm, nj,
-                           ctx->samples.as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
+        hipStream_t as = ms;
+        if(nslots > 1)
+        {
+            as = ctx->acc_stream;
+            PTG_HIP(hipEventRecord(sl.ev_done, ms));
+            PTG_HIP(hipStreamWaitEvent(as, sl.ev_done, 0));
+        }
+        if(int r = timed_begin(ctx, K_ACCUM, as)) return r;
+        hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, as, pm, nj,
+                           sl.samples->as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
                            reinterpret_cast<float4*>(out_accum), reinterpret_cast<uchar4*>(out_bgra));
         PTG_HIP(hipGetLastError());
-        if(int r = timed_end(ctx)) return r;
+        if(int r = timed_end(ctx, as)) return r;
+        if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_acc, as));
+    }
+    if(nslots > 1)
+    {   // the caller's stream sees the whole render
+        PTG_HIP(hipEventRecord(ctx->ev_acc_end, ctx->acc_stream));
+        PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_acc_end, 0));
     }
     if(ctx->counting)
     {
@@ -1099,6 +1173,19 @@ int ptg_context_create(int device, ptg_context** out)
         PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
+        uint32_t slots = PTG_WF_SLOTS;
+        if(const char* v = getenv("PTG_SLOTS")) slots = uint32_t(std::max(1, std::min(2, atoi(v))));
+        if(slots == 2)
+        {
+            ptg_context::Slot& b = ctx->slot[1];
+            PTG_HIP(hipStreamCreateWithFlags(&b.main, hipStreamNonBlocking));
+            PTG_HIP(hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking));
+            PTG_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
+            for(hipEvent_t* e: {&b.ev_main, &b.ev_side, &b.ev_done, &b.ev_acc, &ctx->slot[0].ev_done, &ctx->slot[0].ev_acc,
+                                &ctx->ev_render_start, &ctx->ev_acc_end})
+                PTG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            ctx->nslots = 2;
+        }
     }
     *out = ctx.release();
     return PTG_OK;
