@@ -294,6 +294,21 @@ def main():
             path_ms = elapsed / args.steps * 1e3
             path_bytes = algorithmic_bytes(total)
             traffic, traffic_src = pmc_traffic("extend", workload, ms_per_launch)
+            # the same kernel with nothing beside it: one untimed render with every
+            # kernel on one stream (the timed steps run up to 4 kernels at once)
+            r.set_concurrency(0)
+            r.enable_timing(True)
+            if shard is None:
+                r.render(cfg, out_bgra=image)
+            else:
+                r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+            r.synchronize()
+            kt_iso = r.kernel_times()
+            r.enable_timing(False)
+            r.set_concurrency(2)
+            iso_ms = kt_iso["extend"][0] / max(1, kt_iso["extend"][1])
+            iso_bytes = ext_bytes / max(1, kt_iso["extend"][1])   # one render's bytes over its launches
+            iso_achieved = iso_bytes / (iso_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "traffic_source": traffic_src and ("%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
@@ -302,6 +317,11 @@ def main():
                     "ms_per_launch": round(ms_per_launch, 4), "launches_per_step": ext_n / args.steps,
                     "bytes_per_launch": int(bytes_per_launch),
                     "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_kernel_ms.items()},
+                    "isolated": {"ms_per_launch": round(iso_ms, 4), "achieved": round(iso_achieved, 2),
+                                 "frac": round(iso_achieved / HBM_PEAK_GBS, 5),
+                                 "basis": "one extra untimed render with every kernel on one stream "
+                                          "(ptg_set_concurrency(0)); the timed steps overlap the walk with the sky, "
+                                          "shadow and the other chunk's kernels, which lengthens its launches"},
                     "hot_path": {"achieved_GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
                                  "basis": "wall time per step",
                                  "algorithmic_bytes_per_sample": round(path_bytes / per_step_samples, 1),

@@ -255,6 +255,14 @@ int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8]);
  * bits; PTG_PIPELINE=megakernel selects 1 at context creation. */
 int ptg_set_pipeline(ptg_context* ctx, int pipeline);
 
+/* Concurrency of the wavefront pipeline: 0 = every kernel on the context's
+ * stream; 1 = the sky and shadow kernels on a second stream beside the walks;
+ * 2 (default) = in addition two sample chunks in flight on their own stream
+ * pairs, folded in sample order.  All levels produce identical bits.  Levels
+ * above what the context created (PTG_NO_OVERLAP, PTG_SLOTS) act as the
+ * highest available one. */
+int ptg_set_concurrency(ptg_context* ctx, int level);
+
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);
 

@@ -718,6 +718,7 @@ struct ptg_context {
     };
     Slot slot[2];
     uint32_t nslots = 1;
+    uint32_t concurrency = 2;              // ptg_set_concurrency
     hipStream_t acc_stream = nullptr;
     hipEvent_t ev_render_start = nullptr, ev_acc_end = nullptr;
     ~ptg_context()
@@ -806,7 +807,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     // bounce round then launches over a long queue, so the walk and shade
     // launches run at full occupancy with short tails.  2^28 paths = 93 GB.
     // wavefront chunk pipelines: slot 0 is the context's stream pair and buffers
-    const uint32_t nslots = wf ? ctx->nslots : 1u;
+    const uint32_t nslots = (wf && ctx->concurrency >= 2) ? ctx->nslots : 1u;
     ptg_context::Slot* slots = ctx->slot;
     slots[0].main = ctx->stream;
     slots[0].side = ctx->side;
@@ -891,7 +892,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     }
     const DevScene sc = ctx->scene_args(cfg);
     const uint32_t persistent = ctx->persistent_blocks;
-    const bool overlap = wf && ctx->side != nullptr;
+    const bool overlap = wf && ctx->side != nullptr && ctx->concurrency >= 1;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
     uint32_t chunk_index = 0;
     for(uint32_t j = j0; j < j1; j += chunk, ++chunk_index)
@@ -1552,6 +1553,13 @@ int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8])
     if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_kernel_counters: bad arguments");
     if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable or PTG_COUNTERS=1)");
     memcpy(out, ctx->kind_counters, sizeof(ctx->kind_counters));
+    return PTG_OK;
+}
+
+int ptg_set_concurrency(ptg_context* ctx, int level)
+{
+    if(!ctx || level < 0 || level > 2) return fail(PTG_E_INVALID, "ptg_set_concurrency: 0, 1 or 2");
+    ctx->concurrency = uint32_t(level);
     return PTG_OK;
 }
 

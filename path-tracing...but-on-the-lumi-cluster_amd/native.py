@@ -110,6 +110,7 @@ def lib():
         "ptg_last_kernel_times": (I, [P, P, P]),
         "ptg_last_kernel_counters": (I, [P, P]),
         "ptg_set_pipeline": (I, [P, I]),
+        "ptg_set_concurrency": (I, [P, I]),
         "ptg_synchronize": (I, [P]),
         "ptg_device_alloc": (I, [P, SZ, C.POINTER(P)]),
         "ptg_device_free": (I, [P, P]),

@@ -163,6 +163,11 @@ class GpuRenderer:
         """'wavefront' (default) or 'megakernel' - bit-identical results."""
         N.check(N.lib().ptg_set_pipeline(self._ctx, {"wavefront": 0, "megakernel": 1}[name]), "ptg_set_pipeline")
 
+    def set_concurrency(self, level):
+        """0: one stream; 1: sky/shadow kernels on a second stream; 2 (default):
+        also two sample chunks in flight.  Identical bits at every level."""
+        N.check(N.lib().ptg_set_concurrency(self._ctx, int(level)), "ptg_set_concurrency")
+
     def enable_counters(self, on=True):
         N.check(N.lib().ptg_counters_enable(self._ctx, 1 if on else 0), "ptg_counters_enable")
 

@@ -108,3 +108,24 @@ def test_pipelines_identical(gpu, assets_dir):
     gpu.set_pipeline("wavefront")
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(_bits(outs[0][1]), _bits(outs[1][1]))
+
+
+def test_concurrency_levels_identical(gpu, assets_dir):
+    """One stream, two streams, and two sample chunks in flight (the default)
+    give the same bits; at 64 spp the frame is cut into two chunks, which the
+    two chunk pipelines render concurrently and fold in sample order."""
+    W, H, SPP = 640, 360, 64
+    s = scene_for(assets_dir, W, H, SPP, frame=450)
+    gpu.upload_arrays(arrays_copy(s))
+    outs = []
+    for level in (0, 1, 2):
+        gpu.set_concurrency(level)
+        bgra, acc = gpu.render(s.cfg, want_accum=True)
+        gpu.synchronize()
+        outs.append((bgra.cpu().numpy(), acc.cpu().numpy()))
+    gpu.set_concurrency(2)
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0])
+        assert np.array_equal(_bits(outs[0][1]), _bits(o[1]))
+    with pytest.raises(Exception):
+        gpu.set_concurrency(3)
