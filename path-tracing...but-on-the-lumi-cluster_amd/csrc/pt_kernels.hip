@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
 #ifndef PTG_REFILL_IDLE
-#define PTG_REFILL_IDLE 16
+#define PTG_REFILL_IDLE 24
 #endif
 constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many lanes are idle
 #ifdef PTG_WALK_WAVES
