@@ -39,7 +39,7 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef PTG_SHADE_WAVES
-#define PTG_SHADE_WAVES 3
+#define PTG_SHADE_WAVES 2
 #endif
 
 // ---------------------------------------------------------------- kernels --
