@@ -716,7 +716,8 @@ struct ptg_context {
         DevBuf* state = nullptr;
         DevBuf* samples = nullptr;
     };
-    Slot slot[2];
+    static constexpr uint32_t kMaxSlots = 3;
+    Slot slot[kMaxSlots];
     uint32_t nslots = 1;
     uint32_t concurrency = 2;              // ptg_set_concurrency
     hipStream_t acc_stream = nullptr;
@@ -726,11 +727,20 @@ struct ptg_context {
         if(ev_main) (void)hipEventDestroy(ev_main);
         if(ev_side) (void)hipEventDestroy(ev_side);
         if(side) (void)hipStreamDestroy(side);
-        Slot& b = slot[1];
-        for(hipEvent_t e: {b.ev_main, b.ev_side, b.ev_done, b.ev_acc, slot[0].ev_done, slot[0].ev_acc, ev_render_start, ev_acc_end})
+        for(uint32_t k = 1; k < kMaxSlots; ++k)
+        {
+            Slot& b = slot[k];
+            for(hipEvent_t e: {b.ev_main, b.ev_side})
+                if(e) (void)hipEventDestroy(e);
+            for(hipStream_t st: {b.main, b.side})
+                if(st) (void)hipStreamDestroy(st);
+        }
+        for(uint32_t k = 0; k < kMaxSlots; ++k)
+            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc})
+                if(e) (void)hipEventDestroy(e);
+        for(hipEvent_t e: {ev_render_start, ev_acc_end})
             if(e) (void)hipEventDestroy(e);
-        for(hipStream_t st: {b.main, b.side, acc_stream})
-            if(st) (void)hipStreamDestroy(st);
+        if(acc_stream) (void)hipStreamDestroy(acc_stream);
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
         for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
     }
@@ -815,15 +825,18 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     slots[0].ev_side = ctx->ev_side;
     slots[0].state = &ctx->wf_state;
     slots[0].samples = &ctx->samples;
-    slots[1].state = &slots[1].own_state;
-    slots[1].samples = &slots[1].own_samples;
+    for(uint32_t k = 1; k < ptg_context::kMaxSlots; ++k)
+    {
+        slots[k].state = &slots[k].own_state;
+        slots[k].samples = &slots[k].own_samples;
+    }
     size_t target = (size_t(1) << 30) / sizeof(float4);
     if(wf)
     {
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
         const size_t per_path = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 4 * 4 + sizeof(float4);
-        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * ctx->hbm_pct / per_path));
+        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * (nslots > 2 ? ctx->hbm_pct * 2 / nslots : ctx->hbm_pct) / per_path));
     }
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
     const uint32_t span = j1 - j0;
@@ -852,7 +865,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         uint32_t* lists[2] = {nullptr, nullptr};
         uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
         uint32_t* counts = nullptr;
-    } st[2];
+    } st[ptg_context::kMaxSlots];
     if(wf)
         for(uint32_t k = 0; k < nslots; ++k)
         {
@@ -887,7 +900,8 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     if(nslots > 1)
     {   // the other slot and the accumulation stream start after what the caller queued
         PTG_HIP(hipEventRecord(ctx->ev_render_start, ctx->stream));
-        PTG_HIP(hipStreamWaitEvent(slots[1].main, ctx->ev_render_start, 0));
+        for(uint32_t k = 1; k < nslots; ++k)
+            PTG_HIP(hipStreamWaitEvent(slots[k].main, ctx->ev_render_start, 0));
         PTG_HIP(hipStreamWaitEvent(ctx->acc_stream, ctx->ev_render_start, 0));
     }
     const DevScene sc = ctx->scene_args(cfg);
@@ -1175,17 +1189,27 @@ int ptg_context_create(int device, ptg_context** out)
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
         uint32_t slots = PTG_WF_SLOTS;
-        if(const char* v = getenv("PTG_SLOTS")) slots = uint32_t(std::max(1, std::min(2, atoi(v))));
-        if(slots == 2)
+        if(const char* v = getenv("PTG_SLOTS"))
+            slots = uint32_t(std::max(1, std::min(int(ptg_context::kMaxSlots), atoi(v))));
+        if(slots > 1)
         {
-            ptg_context::Slot& b = ctx->slot[1];
-            PTG_HIP(hipStreamCreateWithFlags(&b.main, hipStreamNonBlocking));
-            PTG_HIP(hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking));
+            for(uint32_t k = 1; k < slots; ++k)
+            {
+                ptg_context::Slot& b = ctx->slot[k];
+                PTG_HIP(hipStreamCreateWithFlags(&b.main, hipStreamNonBlocking));
+                PTG_HIP(hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking));
+                PTG_HIP(hipEventCreateWithFlags(&b.ev_main, hipEventDisableTiming));
+                PTG_HIP(hipEventCreateWithFlags(&b.ev_side, hipEventDisableTiming));
+            }
+            for(uint32_t k = 0; k < slots; ++k)
+            {
+                PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_done, hipEventDisableTiming));
+                PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_acc, hipEventDisableTiming));
+            }
             PTG_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
-            for(hipEvent_t* e: {&b.ev_main, &b.ev_side, &b.ev_done, &b.ev_acc, &ctx->slot[0].ev_done, &ctx->slot[0].ev_acc,
-                                &ctx->ev_render_start, &ctx->ev_acc_end})
-                PTG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-            ctx->nslots = 2;
+            PTG_HIP(hipEventCreateWithFlags(&ctx->ev_render_start, hipEventDisableTiming));
+            PTG_HIP(hipEventCreateWithFlags(&ctx->ev_acc_end, hipEventDisableTiming));
+            ctx->nslots = slots;
         }
     }
     *out = ctx.release();
