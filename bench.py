@@ -273,6 +273,8 @@ def main():
         roof = None
         if not args.no_roofline:
             # deterministic work counters of the same render (separate counting pass, untimed)
+            if long_steps:
+                print("counting pass", file=sys.stderr, flush=True)
             r.enable_counters(True)
             if shard is None:
                 r.render(cfg, out_bgra=image)
@@ -296,6 +298,8 @@ def main():
             traffic, traffic_src = pmc_traffic("extend", workload, ms_per_launch)
             # the same kernel with nothing beside it: one untimed render with every
             # kernel on one stream (the timed steps run up to 4 kernels at once)
+            if long_steps:
+                print("isolated-walk pass", file=sys.stderr, flush=True)
             r.set_concurrency(0)
             r.enable_timing(True)
             if shard is None:
