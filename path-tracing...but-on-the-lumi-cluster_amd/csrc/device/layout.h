@@ -23,6 +23,14 @@
 
 namespace ptg {
 
+// Non-temporal (streaming) accesses for data that passes through once per
+// round - path state, trace results, per-sample results - so that it does not
+// evict BVH records from L2 and the Infinity Cache.  1: the walks' accesses;
+// 2: every kernel's path state; 3 (default): also the per-sample results.
+// Measured at 1024 spp: frame 0 -1.3%, frame 450 -1.1% (levels 2 and 3 alike).
+#ifndef PTG_NT_STATE
+#define PTG_NT_STATE 3
+#endif
 #ifndef PTG_PAIR_NODES
 #define PTG_PAIR_NODES 1
 #endif

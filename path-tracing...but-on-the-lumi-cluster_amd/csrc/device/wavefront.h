@@ -74,32 +74,63 @@ struct PathRec {
 
 PTG_D f3 xyz(float4 v) { return V3(v.x, v.y, v.z); }
 
+#if PTG_NT_STATE >= 2
+// path state read and written once per round: non-temporal (PTG_NT_STATE 2)
+template<typename T> PTG_D T ld_state(const T* p)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    T out;
+    __builtin_memcpy(&out, &v, 16);
+    return out;
+}
+template<typename T> PTG_D void st_state(T* p, T value)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u v;
+    __builtin_memcpy(&v, &value, 16);
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+}
+#else
+template<typename T> PTG_D T ld_state(const T* p) { return *p; }
+template<typename T> PTG_D void st_state(T* p, T value) { *p = value; }
+#endif
+// per-sample results (written once by shade / sky / camera, read once by k_accumulate)
+#if PTG_NT_STATE >= 3
+template<typename T> PTG_D T ld_out(const T* p) { return ld_state(p); }
+template<typename T> PTG_D void st_out(T* p, T value) { st_state(p, value); }
+#else
+template<typename T> PTG_D T ld_out(const T* p) { return *p; }
+template<typename T> PTG_D void st_out(T* p, T value) { *p = value; }
+#endif
+
 PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
 {
-    S.meta[q] = p.meta;
-    S.seed[q] = p.seed;
-    S.ray_o[q] = make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, 0.f);
-    S.ray_d[q] = make_float4(p.ray_d.x, p.ray_d.y, p.ray_d.z, 0.f);
-    S.att[q] = make_float4(p.att.x, p.att.y, p.att.z, p.reg);
-    S.contrib[q] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf);
-    S.batt[q] = make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f);
-    S.nee_c[q] = make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf);
-    S.nee_d[q] = make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter);
+    st_state(S.meta + q, p.meta);
+    st_state(S.seed + q, p.seed);
+    st_state(S.ray_o + q, make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, 0.f));
+    st_state(S.ray_d + q, make_float4(p.ray_d.x, p.ray_d.y, p.ray_d.z, 0.f));
+    st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
+    st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
+    st_state(S.batt + q, make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f));
+    st_state(S.nee_c + q, make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf));
+    st_state(S.nee_d + q, make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter));
 }
 
 PTG_D PathRec load_path(const PathSoA& S, uint32_t q)
 {
     PathRec p;
-    p.meta = S.meta[q];
-    p.seed = S.seed[q];
-    p.ray_o = xyz(S.ray_o[q]);
-    p.ray_d = xyz(S.ray_d[q]);
-    const float4 a = S.att[q], c = S.contrib[q], nc = S.nee_c[q], nd = S.nee_d[q];
+    p.meta = ld_state(S.meta + q);
+    p.seed = ld_state(S.seed + q);
+    p.ray_o = xyz(ld_state(S.ray_o + q));
+    p.ray_d = xyz(ld_state(S.ray_d + q));
+    const float4 a = ld_state(S.att + q), c = ld_state(S.contrib + q), nc = ld_state(S.nee_c + q),
+                 nd = ld_state(S.nee_d + q);
     p.att = xyz(a);
     p.reg = a.w;
     p.contrib = xyz(c);
     p.bpdf = c.w;
-    p.batt = xyz(S.batt[q]);
+    p.batt = xyz(ld_state(S.batt + q));
     p.nee.color = xyz(nc);
     p.nee.mis_pdf = nc.w;
     p.nee.dir = xyz(nd);
@@ -143,7 +174,7 @@ PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occlude
     }
     if(KIND == 2 || !(round < sc.max_bounces && info.thit > 0))
     {
-        out_samples[p.meta.x] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f);
+        st_out(out_samples + p.meta.x, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f));
         return false;
     }
     // bounce `round` (path_tracer.hh:699-720): NEE setup, BSDF sample, next ray

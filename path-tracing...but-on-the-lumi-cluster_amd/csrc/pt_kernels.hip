@@ -180,6 +180,23 @@ struct PixelMap {
     }
 };
 
+// 16-byte non-temporal load / store of a float4 or uint4 record
+template<typename T> __device__ __forceinline__ T nt_load(const T* p)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    T out;
+    __builtin_memcpy(&out, &v, 16);
+    return out;
+}
+template<typename T> __device__ __forceinline__ void nt_store(T* p, T value)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u v;
+    __builtin_memcpy(&v, &value, 16);
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
 {
     unsigned long long s = v;
@@ -231,10 +248,10 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
         const uint32_t slot = in_chunk ? jj * pm.npix + p : 0xFFFFFFFFu;
         if(!live)
         {
-            if(in_chunk) out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-            S.meta[i] = make_uint4(slot, META_DEAD, 0u, 0u);
-            S.ray_o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            S.ray_d[i] = make_float4(0.f, 0.f, 1.f, 0.f);
+            if(in_chunk) st_out(out + slot, make_float4(0.f, 0.f, 0.f, 0.f));
+            st_state(S.meta + i, make_uint4(slot, META_DEAD, 0u, 0u));
+            st_state(S.ray_o + i, make_float4(0.f, 0.f, 0.f, 0.f));
+            st_state(S.ray_d + i, make_float4(0.f, 0.f, 1.f, 0.f));
             continue;
         }
         const int32_t j = (int32_t)(j0 + jj);
@@ -242,11 +259,11 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
         u4 seed;
         f3 o, d;
         camera_ray(sc, sf, x, y, j, seed, o, d);
-        S.meta[i] = make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE), rd_u(sf, SF_TLAS),
-                               rd_u(sf, SF_TLAS + 4));
-        S.seed[i] = to_uint4(seed);
-        S.ray_o[i] = make_float4(o.x, o.y, o.z, 0.f);
-        S.ray_d[i] = make_float4(d.x, d.y, d.z, 0.f);
+        st_state(S.meta + i, make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE),
+                                        rd_u(sf, SF_TLAS), rd_u(sf, SF_TLAS + 4)));
+        st_state(S.seed + i, to_uint4(seed));
+        st_state(S.ray_o + i, make_float4(o.x, o.y, o.z, 0.f));
+        st_state(S.ray_d + i, make_float4(d.x, d.y, d.z, 0.f));
         ++lives;
     }
     if(COUNT) flush_counters(Counters{}, counters, lives);
@@ -332,8 +349,16 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                     if(v < end && t < n)
                     {
                         q = ANY ? list[t] : t;
+#if PTG_NT_STATE
+                        // path state streams once through the caches: non-temporal, so it
+                        // does not evict BVH records from L2 / the Infinity Cache
+                        const uint4 m = nt_load(S.meta + q);
+                        w.init(sc, m.z, m.w, xyz(nt_load(S.ray_o + q)), ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)),
+                               tmin, tmax);
+#else
                         const uint4 m = S.meta[q];
                         w.init(sc, m.z, m.w, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
+#endif
                         active = true;
                         if(COUNT) cnt.queries++;
                     }
@@ -350,12 +375,21 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             const int r = w.template step<ANY, COUNT>(sc, cnt);
             if(r != 0)
             {
+#if PTG_NT_STATE
+                if(ANY) __builtin_nontemporal_store(r == 2 ? 1u : 0u, tr.shadow + q);
+#else
                 if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
+#endif
                 else
                 {
                     const Hit h = w.result();
+#if PTG_NT_STATE
+                    nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
+                    nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
+#else
                     tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
                     tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
+#endif
                 }
                 active = false;
             }
@@ -429,8 +463,8 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
                                             bool& occluded)
 {
     p = load_path(cur, q);
-    const uint4 hv = tr.hit[q];
-    const float4 bv = tr.bary[q];
+    const uint4 hv = ld_state(tr.hit + q);
+    const float4 bv = ld_state(tr.bary + q);
     h.thit = __uint_as_float(hv.x);
     h.instance_id = hv.y;
     h.primitive_id = hv.z;
@@ -563,7 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelMap pm, uint32_t nj,
     }
     for(uint32_t j = 0; j < nj; ++j)
     {
-        const float4 s = samples[size_t(j) * pm.npix + p];
+        const float4 s = ld_out(samples + size_t(j) * pm.npix + p);
         ax = ax + s.x;
         ay = ay + s.y;
         az = az + s.z;
