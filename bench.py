@@ -47,10 +47,15 @@ def pmc_traffic(kind, workload, ms_per_launch):
     FETCH_SIZE x 1 KiB x 2 (gfx950 correction) + WRITE_SIZE x 1 KiB.  A
     profile counts only if its kernel-trace average launch time agrees with the
     live measurement within 15% (a profile of older code or another chunking
-    is not used); None when no profile qualifies."""
+    is not used), the newest (by profile name) when several do; None when
+    none does."""
     import glob
+    import re
+
+    def natural(path):   # r01_wavefront11 after r01_wavefront9
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
     best = None
-    for f in sorted(glob.glob(os.path.join(PROFILES, "*", "pmc_summary.json"))):
+    for f in sorted(glob.glob(os.path.join(PROFILES, "*", "pmc_summary.json")), key=natural):
         try:
             with open(f) as fh:
                 prof = json.load(fh)
@@ -59,7 +64,7 @@ def pmc_traffic(kind, workload, ms_per_launch):
                 continue
             if abs(ent["trace_avg_ms"] - ms_per_launch) > 0.15 * ms_per_launch:
                 continue
-            best = (int(ent["derived"]["hbm_side_bytes"]), os.path.relpath(f, ROOT))
+            best = (int(ent["derived"]["hbm_side_bytes"]), os.path.relpath(f, ROOT))   # the newest that qualifies
         except (OSError, KeyError, ValueError, TypeError):
             continue
     return best if best else (None, None)
