@@ -529,11 +529,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
 // (path_tracer.hh:456-588), retire.  No survivors.
-#ifdef PTG_SKY_WAVES
-#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
-#else
-#define PTG_SKY_ATTR
+#ifndef PTG_SKY_WAVES
+#define PTG_SKY_WAVES 8     // 64 VGPRs: one sky wave fits beside 7 walk waves per SIMD (see ptg_context_create)
 #endif
+#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr,
                                                    const uint32_t* __restrict__ sky_list,
@@ -1187,11 +1186,12 @@ int ptg_context_create(int device, ptg_context** out)
     // walk grids: a multiple of what is resident at once (the queue is split
     // statically over the waves of the whole grid)
 #if PTG_WALK_LDS
-    // Walk residency: the walks' VGPRs (64) allow 8 blocks/CU, but at 8 the
-    // sky and shade kernels on the other stream cannot get a wave onto a
+    // Walk residency: the walks' VGPRs (60-64) allow 8 blocks/CU, but at 8
+    // the sky and shade kernels on the other streams cannot get a wave onto a
     // SIMD until walk waves retire.  The walk blocks' LDS (cold state padded)
-    // sets how many are resident: 6 (default) leaves 128 VGPRs per SIMD free.
-    uint32_t resident[2] = {6, 6};
+    // sets how many are resident: 7 (default) leaves 64 VGPRs per SIMD, one
+    // sky wave (PTG_SKY_WAVES 8 = 64 VGPRs).
+    uint32_t resident[2] = {7, 7};
     if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
