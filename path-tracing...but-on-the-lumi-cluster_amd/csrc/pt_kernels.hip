@@ -869,7 +869,14 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
         const size_t per_path = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 4 * 4 + sizeof(float4);
-        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, total_b / 100 * (nslots > 2 ? ctx->hbm_pct * 2 / nslots : ctx->hbm_pct) / per_path));
+        // a slot's share of HBM, but never more than what is actually free (other
+        // tenants, torch's cache): buffers this context already holds count as free
+        size_t held = 0;
+        for(uint32_t k = 0; k < nslots; ++k)
+            held += slots[k].state->bytes + slots[k].samples->bytes;
+        const size_t share = total_b / 100 * (nslots > 2 ? ctx->hbm_pct * 2 / nslots : ctx->hbm_pct);
+        const size_t avail = (free_b + held) / 100 * 85 / nslots;
+        target = std::max<size_t>(size_t(1) << 16, std::min(size_t(1) << ctx->chunk_log2, std::min(share, avail) / per_path));
     }
     // equal chunks of whole motion-blur groups (multiples of 8 samples), each <= target paths
     const uint32_t span = j1 - j0;

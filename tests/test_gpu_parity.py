@@ -129,3 +129,32 @@ def test_concurrency_levels_identical(gpu, assets_dir):
         assert np.array_equal(_bits(outs[0][1]), _bits(o[1]))
     with pytest.raises(Exception):
         gpu.set_concurrency(3)
+
+
+def test_chunks_fit_free_memory(gpu, assets_dir):
+    """With most of HBM taken by another tenant (a torch tensor here), a fresh
+    context sizes its chunks to what is free instead of failing, and the frame
+    comes out with the same bits (more, smaller chunks fold in sample order)."""
+    import torch
+    from ptlumi.renderer import GpuRenderer
+    W, H, SPP = 640, 360, 64
+    s = scene_for(assets_dir, W, H, SPP, frame=450)
+    gpu.upload_arrays(arrays_copy(s))
+    bgra0, acc0 = gpu.render(s.cfg, want_accum=True)
+    gpu.synchronize()
+    want = (bgra0.cpu().numpy(), acc0.cpu().numpy())
+    del bgra0, acc0
+    free, _ = torch.cuda.mem_get_info()
+    hog = torch.empty(max(0, free - (6 << 30)), dtype=torch.uint8, device="cuda:0")
+    r = GpuRenderer(0)
+    try:
+        r.upload_arrays(arrays_copy(s))
+        bgra, acc = r.render(s.cfg, want_accum=True)
+        r.synchronize()
+        assert np.array_equal(want[0], bgra.cpu().numpy())
+        assert np.array_equal(_bits(want[1]), _bits(acc.cpu().numpy()))
+        del bgra, acc
+    finally:
+        r.close()
+        del hog
+        torch.cuda.empty_cache()
