@@ -158,3 +158,25 @@ def test_chunks_fit_free_memory(gpu, assets_dir):
         r.close()
         del hog
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("w,h,spp,bounces,frame,rect,samples", [
+    (67, 43, 13, 4, 300, None, None),            # ragged image, spp not a multiple of the 8-sample group
+    (33, 17, 5, 0, 450, None, None),             # camera ray + sky/shading only, no bounce
+    (50, 29, 9, 1, 1000, (7, 3, 31, 19), None),  # one bounce, a rectangle off the origin
+    (41, 23, 24, 7, 1750, None, (3, 21)),        # deep paths, a sample range across group borders
+])
+def test_ragged_configs_bit_exact(gpu, assets_dir, w, h, spp, bounces, frame, rect, samples):
+    """Sizes, sample counts and bounce limits off the power-of-two grid the
+    kernels tile by: the accumulated radiance bits and BGRA bytes equal the
+    oracle's baseline_render over the same rectangle and sample range."""
+    s = scene_for(assets_dir, w, h, spp, bounces=bounces, frame=frame)
+    arr = arrays_copy(s)
+    gpu.upload_arrays(arr)
+    x0, y0, rw, rh = rect if rect else (0, 0, w, h)
+    j0, j1 = samples if samples else (0, spp)
+    bgra, acc = gpu.render(s.cfg, rect=rect, samples=samples, want_accum=True)
+    gpu.synchronize()
+    acc_o, bgra_o = Oracle(arr, s.cfg).render_rect(x0, y0, rw, rh, j0, j1)
+    assert np.array_equal(_bits(acc.cpu().numpy()[..., :3]), _bits(acc_o[..., :3]))
+    assert np.array_equal(bgra.cpu().numpy(), bgra_o)

@@ -14,6 +14,7 @@ ap.add_argument("--height", type=int, default=720)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--pipeline", default="wavefront")
 ap.add_argument("--counters", action="store_true")
+ap.add_argument("--concurrency", type=int, default=2)
 a = ap.parse_args()
 import torch  # noqa
 import ptlumi_loader  # noqa
@@ -21,7 +22,7 @@ from ptlumi import native as N
 from ptlumi.renderer import GpuRenderer
 cfg = N.RenderConfig.make(a.width, a.height, a.spp, a.bounces)
 s = N.Scene(os.path.join(ROOT, "assets"), cfg); s.setup_frame(a.frame)
-r = GpuRenderer(0); r.upload(s); r.set_pipeline(a.pipeline)
+r = GpuRenderer(0); r.upload(s); r.set_pipeline(a.pipeline); r.set_concurrency(a.concurrency)
 img, _ = r.render(cfg); r.synchronize()
 r.enable_timing(True)
 best, kt = 1e30, None
