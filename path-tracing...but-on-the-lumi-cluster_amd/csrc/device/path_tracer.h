@@ -23,6 +23,16 @@ constexpr float EARTH_RADIUS = 6.3781e6f;
 constexpr float ATMOSPHERE_HEIGHT = 1.0e5f;
 constexpr float RAYLEIGH_SCALE_HEIGHT = 7994.0f;
 constexpr float MIE_SCALE_HEIGHT = 1200.0f;
+#ifndef PTG_FAST_DIV
+#define PTG_FAST_DIV 1   // -height / scale height via div_by (== the IEEE division for every float, ref_math.h)
+#endif
+#if PTG_FAST_DIV
+PTG_D float ray_h(float h) { return div_by(-h, RAYLEIGH_SCALE_HEIGHT, 1.0f / RAYLEIGH_SCALE_HEIGHT); }
+PTG_D float mie_h(float h) { return div_by(-h, MIE_SCALE_HEIGHT, 1.0f / MIE_SCALE_HEIGHT); }
+#else
+PTG_D float ray_h(float h) { return -h / RAYLEIGH_SCALE_HEIGHT; }
+PTG_D float mie_h(float h) { return -h / MIE_SCALE_HEIGHT; }
+#endif
 constexpr float MIE_ANISOTROPY = 0.80f;
 constexpr float MIN_RAY_DIST = 1e-4f;
 constexpr float MAX_RAY_DIST = 1e9f;
@@ -673,8 +683,8 @@ PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
     {
         const float t = segment * (jitter + (float)i);
         const float height = length((pos + t * view) - earth) - EARTH_RADIUS;
-        ray_depth = (float)((double)ray_depth + dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)));
-        mie_depth = (float)((double)mie_depth + dexp((double)(-height / MIE_SCALE_HEIGHT)));
+        ray_depth = (float)((double)ray_depth + dexp((double)ray_h(height)));
+        mie_depth = (float)((double)mie_depth + dexp((double)mie_h(height)));
         if(height < 0) shadowed = true;
     }
     if(shadowed) return V3(0.0f, 0.0f, 0.0f);
@@ -718,13 +728,13 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
         {
             const float tt = light_segment * (jitter.y + (float)j);
             const float height = length((p + tt * L.dir) - earth) - EARTH_RADIUS;
-            lray = (float)((double)lray + dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)));
-            lmie = (float)((double)lmie + dexp((double)(-height / MIE_SCALE_HEIGHT)));
+            lray = (float)((double)lray + dexp((double)ray_h(height)));
+            lmie = (float)((double)lmie + dexp((double)mie_h(height)));
             if(height < 0) shadowed = true;
         }
         const float height = gmax(length(p - earth) - EARTH_RADIUS, 0.0f);
-        const float ray_density = (float)(dexp((double)(-height / RAYLEIGH_SCALE_HEIGHT)) * (double)segment);
-        const float mie_density = (float)(dexp((double)(-height / MIE_SCALE_HEIGHT)) * (double)segment);
+        const float ray_density = (float)(dexp((double)ray_h(height)) * (double)segment);
+        const float mie_density = (float)(dexp((double)mie_h(height)) * (double)segment);
         ray_depth += ray_density;
         mie_depth += mie_density;
         const float kr = lray * light_segment + ray_depth, km = lmie * light_segment + mie_depth;

@@ -66,6 +66,23 @@ PTG_D float rcp_rn(float x)
     return ok ? r : 1.0f / x;
 }
 
+// x / c for a divisor c known at compile time, with rc = RN(1/c): the
+// product q1 = RN(x * rc) is within an ulp of the quotient, its residual
+// x - q1 * c is exact by FMA, and one correction step gives the correctly
+// rounded quotient (Markstein) as long as nothing underflows.  So zeros,
+// denormals and other tiny x (|x| < 2^-100), and NaN, take the IEEE division;
+// a zero residual means q1 is exact, and a non-finite one means x is inf,
+// where q1 is already the answer.  tools/div_exhaustive.hip checks every one
+// of the 2^32 inputs against x / c on the GPU for each divisor used.
+PTG_D float div_by(float x, float c, float rc)
+{
+    if(!(fabsf(x) >= 0x1p-100f)) return x / c;
+    const float q1 = x * rc;
+    const float r = __builtin_fmaf(-q1, c, x);
+    const float q = __builtin_fmaf(r, rc, q1);
+    return __builtin_amdgcn_classf(r, 0x198) ? q : q1;   // finite, non-zero residual
+}
+
 // f32 sqrt: correctly rounded == the reference's (float)sqrt((double)x)
 PTG_D float fsqrt(float x) { return __builtin_sqrtf(x); }
 PTG_D float length(f3 a) { return fsqrt(dot(a, a)); }
