@@ -48,7 +48,7 @@ PTG_D f3 cross(f3 a, f3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * 
 // the hardware reciprocal (about 1 ulp) plus one Newton step with FMA gives the
 // correctly rounded reciprocal for every x whose reciprocal is a normal
 // number; the rest (zeros, denormals, |x| >= 2^126, inf, NaN) take the
-// division.  tools/rcp_exhaustive.hip checks all 2^32 inputs against 1.0f / x
+// division.  tools/exhaustive.hip checks all 2^32 inputs against 1.0f / x
 // on the GPU, bit for bit.
 // rcp_nr(x, ok): the fast path alone; ok is cleared when x is outside its
 // range, and the caller then takes the division (one branch for several).
@@ -72,7 +72,7 @@ PTG_D float rcp_rn(float x)
 // rounded quotient (Markstein) as long as nothing underflows.  So zeros,
 // denormals and other tiny x (|x| < 2^-100), and NaN, take the IEEE division;
 // a zero residual means q1 is exact, and a non-finite one means x is inf,
-// where q1 is already the answer.  tools/div_exhaustive.hip checks every one
+// where q1 is already the answer.  tools/exhaustive.hip checks every one
 // of the 2^32 inputs against x / c on the GPU for each divisor used.
 PTG_D float div_by(float x, float c, float rc)
 {
@@ -83,8 +83,34 @@ PTG_D float div_by(float x, float c, float rc)
     return __builtin_amdgcn_classf(r, 0x198) ? q : q1;   // finite, non-zero residual
 }
 
+// sqrt(x), correctly rounded, without the compiler's sequence (v_sqrt_f32,
+// then both ulp neighbours tested by FMA residuals, plus denormal scaling):
+// the hardware 1/sqrt (about 1 ulp), a coupled Newton step on g ~ sqrt(x) and
+// h ~ 1/(2 sqrt(x)), and a final residual correction with FMA.  x outside
+// [2^-100, 2^100] (zeros, denormals, huge values, inf, NaN, negatives) takes
+// the IEEE sqrt in a branch.  tools/exhaustive.hip checks all 2^32 inputs
+// against sqrtf on the GPU, bit for bit.
+PTG_D float sqrt_rn(float x)
+{
+    if(!(x >= 0x1p-100f && x <= 0x1p100f)) return __builtin_sqrtf(x);
+    const float y = __builtin_amdgcn_rsqf(x);
+    float g = x * y, h = 0.5f * y;
+    const float r = __builtin_fmaf(-g, h, 0.5f);
+    g = __builtin_fmaf(g, r, g);
+    h = __builtin_fmaf(h, r, h);
+    const float d = __builtin_fmaf(-g, g, x);
+    return __builtin_fmaf(d, h, g);
+}
+
 // f32 sqrt: correctly rounded == the reference's (float)sqrt((double)x)
+#ifndef PTG_FAST_SQRT
+#define PTG_FAST_SQRT 0   // measured: sky kernel slower with sqrt_rn (frame 0 +1%), see DESIGN.md
+#endif
+#if PTG_FAST_SQRT
+PTG_D float fsqrt(float x) { return sqrt_rn(x); }
+#else
 PTG_D float fsqrt(float x) { return __builtin_sqrtf(x); }
+#endif
 PTG_D float length(f3 a) { return fsqrt(dot(a, a)); }
 PTG_D f3 normalize(f3 a) { return a / length(a); }
 
