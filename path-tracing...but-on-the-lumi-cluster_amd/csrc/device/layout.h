@@ -31,6 +31,12 @@ namespace ptg {
 #ifndef PTG_NT_STATE
 #define PTG_NT_STATE 3
 #endif
+#ifndef PTG_CLASSIFY_FLAG
+#define PTG_CLASSIFY_FLAG 1 // k_wf_classify takes "NEE pending and unoccluded" from the shadow flags alone
+#endif
+#ifndef PTG_NEE_LAZY
+#define PTG_NEE_LAZY 2      // shade/sky read (1) and write (2) a path's NEE records only when it has a pending NEE ray
+#endif
 #ifndef PTG_PAIR_NODES
 #define PTG_PAIR_NODES 1
 #endif

@@ -113,19 +113,45 @@ PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
     st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
     st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
     st_state(S.batt + q, make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f));
+#if PTG_NEE_LAZY >= 2
+    if(!meta_nee(p.meta)) return;   // no pending NEE ray: its records are never read
+#endif
     st_state(S.nee_c + q, make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf));
     st_state(S.nee_d + q, make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter));
 }
 
-PTG_D PathRec load_path(const PathSoA& S, uint32_t q)
+// `carried` = false for round 0 (camera rays): the camera writes only meta,
+// seed and the ray, and shade_path's round-0 branch writes throughput,
+// contribution, bounce and NEE fields before it reads them, so those five
+// records (80 B per path) are not fetched.
+PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
 {
     PathRec p;
     p.meta = ld_state(S.meta + q);
     p.seed = ld_state(S.seed + q);
     p.ray_o = xyz(ld_state(S.ray_o + q));
     p.ray_d = xyz(ld_state(S.ray_d + q));
+    if(!carried)
+    {
+        p.att = p.contrib = p.batt = V3(0, 0, 0);
+        p.reg = p.bpdf = 0;
+        p.nee = NeeCandidate{V3(0, 0, 0), V3(0, 0, 0), 0, 0};
+        return p;
+    }
+#if PTG_NEE_LAZY
+    // the pending NEE candidate is read only by paths that have one (classify
+    // groups those paths together, so a wave mostly takes one side)
+    float4 nc = make_float4(0.f, 0.f, 0.f, 0.f), nd = nc;
+    if(meta_nee(p.meta))
+    {
+        nc = ld_state(S.nee_c + q);
+        nd = ld_state(S.nee_d + q);
+    }
+    const float4 a = ld_state(S.att + q), c = ld_state(S.contrib + q);
+#else
     const float4 a = ld_state(S.att + q), c = ld_state(S.contrib + q), nc = ld_state(S.nee_c + q),
                  nd = ld_state(S.nee_d + q);
+#endif
     p.att = xyz(a);
     p.reg = a.w;
     p.contrib = xyz(c);

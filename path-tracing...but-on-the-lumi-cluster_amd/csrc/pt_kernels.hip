@@ -434,7 +434,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
             if(q < n)
             {
                 const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
+#if PTG_CLASSIFY_FLAG
+                // shade(round-1) wrote 1 for survivors without a pending NEE ray,
+                // the shadow walk 0/1 for those with one (meta is not read)
+                const bool nee = round > 0 && tr.shadow[q] == 0;
+#else
                 const bool nee = round > 0 && meta_nee(meta[q]) && tr.shadow[q] == 0;
+#endif
                 key[k] = (hit ? 2u : 0u) | (nee ? 1u : 0u);
                 rank[k] = atomicAdd(&bin_count[key[k]], 1u);
             }
@@ -460,9 +466,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
 }
 
 __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& tr, uint32_t q, PathRec& p, Hit& h,
-                                            bool& occluded)
+                                            bool& occluded, bool carried)
 {
-    p = load_path(cur, q);
+    p = load_path(cur, q, carried);
     const uint4 hv = ld_state(tr.hit + q);
     const float4 bv = ld_state(tr.bary + q);
     h.thit = __uint_as_float(hv.x);
@@ -481,7 +487,7 @@ template<bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(
     DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
     const uint32_t* __restrict__ hit_list, const uint32_t* __restrict__ lcounts, uint32_t* __restrict__ next_list,
-    float4* __restrict__ out, unsigned long long* __restrict__ counters)
+    uint32_t* __restrict__ next_shadow, float4* __restrict__ out, unsigned long long* __restrict__ counters)
 {
     const uint32_t n = lcounts[0];
     Counters cnt;
@@ -495,7 +501,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         {
             Hit h;
             bool occluded;
-            load_queued(cur, tr, hit_list[i], p, h, occluded);
+            load_queued(cur, tr, hit_list[i], p, h, occluded, round > 0);
             cont = shade_path<COUNT, 1>(sc, p, h, occluded, out, cnt);
             nee = cont && meta_nee(p.meta);
         }
@@ -522,6 +528,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         const uint32_t qn = blk_base + oct_start[okey] + orank;
         if(cont) store_path(nxt, qn, p);
         if(nee) next_list[nee_base + nrank] = qn;
+#if PTG_CLASSIFY_FLAG
+        else if(cont) __builtin_nontemporal_store(1u, next_shadow + qn);   // no NEE ray: k_wf_classify reads "occluded"
+#endif
         __syncthreads();   // the LDS tables are rewritten by the next iteration
     }
     if(COUNT) flush_counters(cnt, counters, 0);
@@ -534,7 +543,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 #endif
 #define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
 template<bool COUNT>
-__global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr,
+__global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr, uint32_t round,
                                                    const uint32_t* __restrict__ sky_list,
                                                    const uint32_t* __restrict__ lcounts, float4* __restrict__ out,
                                                    unsigned long long* __restrict__ counters)
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, Pat
         PathRec p;
         Hit h;
         bool occluded;
-        load_queued(cur, tr, sky_list[i], p, h, occluded);
+        load_queued(cur, tr, sky_list[i], p, h, occluded, round > 0);
         shade_path<COUNT, 2>(sc, p, h, occluded, out, cnt);
     }
     if(COUNT) flush_counters(cnt, counters, 0);
@@ -1035,10 +1044,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
-                                       hit_list, lc, lists[(r + 1) & 1], out, cnt_for(K_SHADE));
+                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, cnt_for(K_SHADE));
                 else
                     hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
-                                       hit_list, lc, lists[(r + 1) & 1], out, nullptr);
+                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
                 // escaped rays retire without feeding the next round: their
@@ -1051,10 +1060,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, sky_list, lc, out,
+                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
                                        cnt_for(K_SHADE));
                 else
-                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, sky_list, lc, out, nullptr);
+                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
             }
