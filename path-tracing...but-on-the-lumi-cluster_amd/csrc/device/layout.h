@@ -31,6 +31,9 @@ namespace ptg {
 #ifndef PTG_NT_STATE
 #define PTG_NT_STATE 3
 #endif
+#ifndef PTG_MISS_BARY
+#define PTG_MISS_BARY 1     // sky kernel: no hit / barycentric reads, walk: no barycentric write for a miss
+#endif
 #ifndef PTG_CLASSIFY_FLAG
 #define PTG_CLASSIFY_FLAG 1 // k_wf_classify takes "NEE pending and unoccluded" from the shadow flags alone
 #endif

@@ -385,7 +385,10 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                     const Hit h = w.result();
 #if PTG_NT_STATE
                     nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
-                    nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
+#if PTG_MISS_BARY
+                    if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
+#endif
+                        nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
 #else
                     tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
                     tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
@@ -465,10 +468,28 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
     }
 }
 
+// MISS: the caller shades a path whose ray left the scene (k_wf_classify put
+// it on the sky list because its hit distance was not positive).  The walk
+// reports such a ray as WalkerT::result() does, thit = -1 and no hit, and the
+// sky branch of shade_path reads nothing else of it: the hit and barycentric
+// records are not fetched (nor, PTG_MISS_BARY, the barycentrics written).
+template<bool MISS = false>
 __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& tr, uint32_t q, PathRec& p, Hit& h,
                                             bool& occluded, bool carried)
 {
     p = load_path(cur, q, carried);
+    occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
+#if PTG_MISS_BARY
+    if(MISS)
+    {
+        h.thit = -1.0f;
+        h.instance_id = 0xFFFFFFFFu;
+        h.primitive_id = 0;
+        h.back_face = false;
+        h.bx = h.by = h.bz = 0.0f;
+        return;
+    }
+#endif
     const uint4 hv = ld_state(tr.hit + q);
     const float4 bv = ld_state(tr.bary + q);
     h.thit = __uint_as_float(hv.x);
@@ -476,7 +497,6 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
     h.primitive_id = hv.z;
     h.back_face = hv.w != 0;
     h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
-    occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
 }
 
 // Surface hits: NEE finish, bounce tail, then NEE setup + BSDF sample of the
@@ -555,7 +575,7 @@ __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, Pat
         PathRec p;
         Hit h;
         bool occluded;
-        load_queued(cur, tr, sky_list[i], p, h, occluded, round > 0);
+        load_queued<true>(cur, tr, sky_list[i], p, h, occluded, round > 0);
         shade_path<COUNT, 2>(sc, p, h, occluded, out, cnt);
     }
     if(COUNT) flush_counters(cnt, counters, 0);
