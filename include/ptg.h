@@ -248,6 +248,12 @@ int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches);
  * [2] shadow (any-hit walk), [3] shade (surface hits), [4] camera,
  * [5] accumulate, [6] sky (rays that left the scene), [7] classify. */
 int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8]);
+/* The same record read as busy time: per kind, the UNION of the recorded
+ * launches' [start, end) intervals on one device time axis (busy_ms), beside
+ * their plain sum (ms) and count.  Launches of one kind that overlap (the two
+ * chunk pipelines) are counted once, so busy_ms never exceeds the wall time
+ * of the recorded renders.  Waits for them and clears the record. */
+int ptg_last_kernel_busy(ptg_context* ctx, double busy_ms[8], double ms[8], uint32_t launches[8]);
 
 /* Execution strategy of ptg_render*: 0 = wavefront pipeline (default:
  * camera / extend / shadow / shade kernels over compacted path queues),

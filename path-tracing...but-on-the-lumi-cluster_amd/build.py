@@ -4,7 +4,8 @@
 kernels for gfx950 and the host C++ (make -C csrc), prepares the scene assets
 and, for the tests only, builds the oracle (oracle/Makefile) - and, when the
 reference tree is present (this container, not the GPU box), the reference
-renderer from its sources as the oracle's checker.  Built files stay in the
+renderer from its sources as the oracle's checker - and the user-kernel test
+library built against include/ptg_device.h.  Built files stay in the
 tree (git-ignored) so they travel to the GPU box with the snapshot.
 """
 from __future__ import annotations
@@ -57,6 +58,12 @@ def build_oracle(verbose=False, jobs=8, with_reference=None):
                   "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
 
 
+def build_test_kernels(verbose=False):
+    """The user-kernel library of tests/test_gpu_device_dropin.py: a HIP kernel
+    built against include/ptg_device.h alone (test infrastructure)."""
+    _run(["make"], os.path.join(ROOT, "tests", "device_dropin"), verbose)
+
+
 def prepare_assets():
     from . import assets
     return assets.prepare(assets.default_dir(ROOT))
@@ -65,4 +72,5 @@ def prepare_assets():
 def build(verbose=False):
     prepare_assets()
     build_native(verbose)
+    build_test_kernels(verbose)
     build_oracle(verbose)

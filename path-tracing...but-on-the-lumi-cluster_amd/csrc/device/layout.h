@@ -94,7 +94,19 @@ struct DevScene {
     const float2* polygon;         // per subframe: (sin, cos) of the aperture polygon's vertex angles (kPolyStride each)
     uint32_t width, height, spp, max_bounces, student_id, blur_step;
     uint32_t subframe_count;
+    // bounds of the record buffers, checked only by PTG_DEBUG builds
+    uint32_t trav_count, tri_count, inst_count;
+    uint32_t* debug;               // PTG_DEBUG: violation counters (kDebug* slots), else null
 };
+
+// PTG_DEBUG builds check every index the walks and the shading derive from
+// the records before they use it; a violation is counted in DevScene::debug
+// (slot below), the walk of that ray ends instead of reading out of bounds,
+// and the render returns PTG_E_RANGE naming the slot.
+#ifndef PTG_DEBUG
+#define PTG_DEBUG 0
+#endif
+enum : uint32_t { kDebugNode = 0, kDebugTri = 1, kDebugInst = 2, kDebugQueue = 3, kDebugList = 4, kDebugSlots = 8 };
 
 // Aperture polygons with at most kPolyMaxSides sides read their vertex
 // directions from DevScene::polygon (k_polygon_table).

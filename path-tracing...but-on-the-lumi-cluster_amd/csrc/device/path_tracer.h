@@ -41,6 +41,19 @@ constexpr int PRIMARY_ITERATIONS = 8;
 constexpr int SECONDARY_ITERATIONS = 4;
 
 // Work counters (only in the counting build of a kernel).
+#if PTG_DEBUG
+#define PTG_CHECK(sc, cond, slot)                                     \
+    do {                                                              \
+        if(!(cond))                                                   \
+        {                                                             \
+            if((sc).debug) atomicAdd((sc).debug + (slot), 1u);        \
+            return 1;                                                 \
+        }                                                             \
+    } while(0)
+#else
+#define PTG_CHECK(sc, cond, slot) do {} while(0)
+#endif
+
 struct Counters {
     uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0, iters = 0;
 };
@@ -67,6 +80,59 @@ PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
     const float4* q = reinterpret_cast<const float4*>(p);
     lo = q[0];
     hi = q[1];
+}
+
+// ray_triangle_intersection (math.hh:358-401) followed by the distance test of
+// ray_query_test_triangle (ray_query.hh:243-245): true when the triangle
+// P0 P1 P2 is an accepted candidate (det != 0, t >= 0, barycentrics of one
+// sign, tmin < t < tmax); u, v, t and back are then the candidate's values.
+// The division-free parts of the acceptance test come first: most tested
+// triangles fail them and then skip the reciprocal.
+PTG_D bool tri_accept(f3 org, int axis, f3 S, f3 P0, f3 P1, f3 P2, float tmin, float tmax, float& u, float& v,
+                      float& t, bool& back)
+{
+    const f3 A = P0 - org, B = P1 - org, C = P2 - org;
+    f3 x = V3(A.x, B.x, C.x), y = V3(A.y, B.y, C.y), z = V3(A.z, B.z, C.z);
+    if(axis == 0) { x = z; z = V3(A.x, B.x, C.x); }
+    else if(axis == 1) { y = z; z = V3(A.y, B.y, C.y); }
+    x = x - S.x * z;
+    y = y - S.y * z;
+    const f3 uvw = cross(y, x);
+    const float det = uvw.x + uvw.y + uvw.z;
+    if(!(det != 0.0f && ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
+                         (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f))))
+        return false;
+    const float rdet = wrcp(det);
+    u = uvw.x * rdet;
+    v = uvw.y * rdet;
+    t = dot(uvw, S.z * z) * rdet;
+    back = det < 0;
+    if(S.z < 0) back = !back;
+    if(axis != 2) back = !back;
+    return t >= 0.0f && t < tmax && t > tmin;
+}
+
+// ray_triangle_intersection_preprocess (math.hh:340-356)
+PTG_D void tri_preprocess(f3 d, int& axis, f3& S)
+{
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    f3 rd = d;
+    axis = 2;
+    if(ax > ay && ax > az) { axis = 0; rd = V3(d.z, d.y, d.x); }
+    else if(ay > az) { axis = 1; rd = V3(d.x, d.z, d.y); }
+    const float k = 1.0f / rd.z;
+    S = V3(rd.x * k, rd.y * k, 1.0f * k);
+}
+
+// slab test of ray_query_traverse (ray_query.hh:197-207)
+PTG_D bool slab_hit(f3 org, f3 inv, float tmin, float tmax, float lx, float ly, float lz, float hx, float hy, float hz)
+{
+    const float t0x = (lx - org.x) * inv.x, t1x = (hx - org.x) * inv.x;
+    const float t0y = (ly - org.y) * inv.y, t1y = (hy - org.y) * inv.y;
+    const float t0z = (lz - org.z) * inv.z, t1z = (hz - org.z) * inv.z;
+    const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
+    const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
+    return nearv <= farv && farv > tmin && nearv < tmax;
 }
 
 // Where a walk keeps its cold state - the world ray, its reciprocal, the
@@ -219,6 +285,7 @@ struct WalkerT {
             cold.leave_blas(org, inv, base, node, count);
             return 0;
         }
+        PTG_CHECK(sc, base + node < sc.trav_count, kDebugNode);
         float4 lo, hi;
         const TravRec* rec = sc.trav + (base + node);
         load_trav(rec, lo, hi);
@@ -248,6 +315,7 @@ struct WalkerT {
         const uint32_t leaf = accept & 0x7FFFFFFFu;
         if(axis < 0)
         {
+            PTG_CHECK(sc, leaf < sc.inst_count, kDebugInst);
             // ray_query_enter_blas (ray_query.hh:153-182)
             if(COUNT) cnt.blas_entries++;
             typedef float v4f __attribute__((ext_vector_type(4)));
@@ -298,27 +366,13 @@ struct WalkerT {
         }
         // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246, math.hh:358-401)
         if(COUNT) cnt.tri_tests++;
+        PTG_CHECK(sc, tri_base + leaf < sc.tri_count, kDebugTri);
         const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + leaf);
         const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-        const f3 A = V3(q0.x, q0.y, q0.z) - org, B = V3(q0.w, q1.x, q1.y) - org, C = V3(q1.z, q1.w, q2.x) - org;
-        f3 x = V3(A.x, B.x, C.x), y = V3(A.y, B.y, C.y), z = V3(A.z, B.z, C.z);
-        if(axis == 0) { x = z; z = V3(A.x, B.x, C.x); }
-        else if(axis == 1) { y = z; z = V3(A.y, B.y, C.y); }
-        x = x - S.x * z;
-        y = y - S.y * z;
-        const f3 uvw = cross(y, x);
-        const float det = uvw.x + uvw.y + uvw.z;
-        // the division-free parts of the acceptance test first: most tested
-        // triangles fail them, and those lanes then skip the IEEE division
-        if(!(det != 0.0f && ((uvw.x >= 0.0f && uvw.y >= 0.0f && uvw.z >= 0.0f) ||
-                             (uvw.x <= 0.0f && uvw.y <= 0.0f && uvw.z <= 0.0f))))
-            return 0;
-        const float rdet = wrcp(det);
-        const float u = uvw.x * rdet, v = uvw.y * rdet, t = dot(uvw, S.z * z) * rdet;
-        bool back = det < 0;
-        if(S.z < 0) back = !back;
-        if(axis != 2) back = !back;
-        if(t >= 0.0f && t < tmax && t > tmin)
+        float u, v, t;
+        bool back;
+        if(tri_accept(org, axis, S, V3(q0.x, q0.y, q0.z), V3(q0.w, q1.x, q1.y), V3(q1.z, q1.w, q2.x), tmin, tmax, u, v, t,
+                      back))
         {
             if(ANY) return 2;
             cold.confirm(u, v, t, inst, leaf, back);
@@ -342,6 +396,151 @@ PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, 
     while((r = w.template step<ANY, COUNT>(sc, cnt)) == 0) {}
     best = w.result();
     return ANY ? r == 2 : best.thit >= 0.0f;
+}
+
+// ---- the same hot path over the reference's own arrays --------------------
+// RefScene holds the nine borrowed pointers of path_trace_pixel
+// (path_tracer.hh:637-654) in the reference layout (bvh.hh, mesh.hh,
+// scene.hh): nodes 24 B, 8 link orders of 8 B per node, indices, 16-byte
+// float3 positions/normals, float4 albedo/material, 160-byte instances and
+// subframes.  trace() over a RefScene walks those arrays exactly as
+// ray_query_proceed does (ray_query.hh:184-278) - no repacking - so a kernel
+// can call path_trace_pixel on the arrays the reference's scene holds
+// (include/ptg_device.h).  The frame renderer uses DevScene's repacked records.
+struct RefScene {
+    const uint8_t* subframes;        // subframe[]          (160 B)
+    const uint8_t* instances;        // tlas_instance[]     (160 B)
+    const float* nodes;              // bvh_node[]          (24 B)
+    const uint2* links;              // bvh_link[], 8 orders per node
+    const uint32_t* indices;
+    const float* pos;                // float3[] (16 B stride)
+    const float* normal;
+    const float* albedo;             // float4[]
+    const float* material;
+    const float2* polygon;           // always null: the camera evaluates the aperture polygon itself
+    uint32_t width, height, max_bounces, student_id, blur_step;
+};
+
+// ray_query_context (ray_query.hh:52-60)
+struct RefLevel {
+    uint32_t count, offset, link_offset, node;
+    f3 org, inv;
+};
+
+// ray_query_traverse (ray_query.hh:184-223): next leaf payload, or 0xFFFFFFFF
+PTG_D uint32_t ref_traverse(const RefScene& sc, RefLevel& c, float tmin, float tmax, Counters& cnt, bool count)
+{
+    while(c.node < c.count)
+    {
+        const float* n = sc.nodes + size_t(c.offset + c.node) * 6;
+        const uint2 l = sc.links[c.link_offset + c.node];
+        if(count) cnt.visits++;
+        if(slab_hit(c.org, c.inv, tmin, tmax, n[0], n[1], n[2], n[3], n[4], n[5]))
+        {
+            const uint32_t accept = l.x & 0x7FFFFFFFu;
+            if(accept != l.x) { c.node = l.y; return accept; }
+            c.node = accept;
+        }
+        else c.node = l.y;
+    }
+    return 0xFFFFFFFFu;
+}
+
+PTG_D f3 ref_f3(const float* base, uint32_t i)
+{
+    const float4 v = reinterpret_cast<const float4*>(base)[i];
+    return V3(v.x, v.y, v.z);
+}
+
+// ray_query_initialize + the proceed/confirm loop of trace_ray (ANY = false,
+// path_tracer.hh:342-349) or the single proceed of trace_shadow_ray (ANY =
+// true, :415-427), over the reference arrays.
+template<bool ANY, bool COUNT>
+PTG_D bool trace(const RefScene& sc, uint32_t tlas_count, uint32_t tlas_offset, f3 o, f3 d, float tmin, float tmax,
+                 Hit& best, Counters& cnt)
+{
+    if(COUNT) cnt.queries++;
+    RefLevel tl{tlas_count, tlas_offset, tlas_offset * 8 + octant(d) * tlas_count, 0, o,
+                V3(rcp_or_big(d.x), rcp_or_big(d.y), rcp_or_big(d.z))};
+    RefLevel bl{0, 0, 0, 0, V3(0, 0, 0), V3(0, 0, 0)};
+    int axis = -1;
+    f3 S = V3(0, 0, 0);
+    uint32_t inst = 0xFFFFFFFFu, ioff = 0, bv = 0;
+    best.thit = -1.0f;
+    best.bx = best.by = best.bz = 0.0f;
+    best.instance_id = 0xFFFFFFFFu;
+    best.primitive_id = 0;
+    best.back_face = false;
+    for(;;)
+    {
+        const uint32_t leaf = ref_traverse(sc, axis < 0 ? tl : bl, tmin, tmax, cnt, COUNT);
+        if(leaf == 0xFFFFFFFFu)
+        {
+            if(axis < 0) return ANY ? false : best.thit >= 0.0f;
+            axis = -1;
+            continue;
+        }
+        if(axis < 0)
+        {   // ray_query_enter_blas (ray_query.hh:153-182)
+            if(COUNT) cnt.blas_entries++;
+            const uint8_t* in = sc.instances + size_t(leaf) * 160;
+            const uint32_t* h = reinterpret_cast<const uint32_t*>(in);
+            const float* M = reinterpret_cast<const float*>(in + 96);      // inv_transform rows
+            bl.count = h[0];
+            bl.offset = h[1];
+            ioff = h[4];
+            bv = h[5];
+            inst = leaf;
+            bl.org = V3(M[0] * o.x + M[4] * o.y + M[8] * o.z + M[12] * 1.0f,
+                        M[1] * o.x + M[5] * o.y + M[9] * o.z + M[13] * 1.0f,
+                        M[2] * o.x + M[6] * o.y + M[10] * o.z + M[14] * 1.0f);
+            const f3 bd = V3(M[0] * d.x + M[4] * d.y + M[8] * d.z, M[1] * d.x + M[5] * d.y + M[9] * d.z,
+                             M[2] * d.x + M[6] * d.y + M[10] * d.z);
+            bl.inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+            bl.link_offset = bl.offset * 8 + octant(bd) * bl.count;
+            bl.node = 0;
+            tri_preprocess(bd, axis, S);
+            continue;
+        }
+        // ray_query_test_triangle (ray_query.hh:225-246)
+        if(COUNT) cnt.tri_tests++;
+        const uint32_t* tri = sc.indices + ioff + leaf * 3;
+        float u, v, t;
+        bool back;
+        if(tri_accept(bl.org, axis, S, ref_f3(sc.pos, bv + tri[0]), ref_f3(sc.pos, bv + tri[1]), ref_f3(sc.pos, bv + tri[2]),
+                      tmin, tmax, u, v, t, back))
+        {
+            if(ANY) return true;
+            // ray_query_confirm (ray_query.hh:280-290)
+            best.bx = u;
+            best.by = v;
+            best.bz = 1.0f - u - v;
+            best.thit = t;
+            best.instance_id = inst;
+            best.primitive_id = leaf;
+            best.back_face = back;
+            tmax = t;
+        }
+    }
+}
+
+// Where the shading of a hit finds its instance: the transform's rotation
+// rows (extract_m4m3) and the mesh's index / vertex offsets (path_tracer.hh:369-371).
+PTG_D void shade_instance(const DevScene& sc, uint32_t id, m3& rot, uint32_t& ioff, uint32_t& bv)
+{
+    const float4* sp = reinterpret_cast<const float4*>(sc.inst_shade + id);
+    const float4 s0 = sp[0], s1 = sp[1], s2 = sp[2];
+    rot = m3{{V3(s0.x, s0.y, s0.z), V3(s0.w, s1.x, s1.y), V3(s1.z, s1.w, s2.x)}};
+    ioff = __float_as_uint(s2.y);
+    bv = __float_as_uint(s2.z);
+}
+PTG_D void shade_instance(const RefScene& sc, uint32_t id, m3& rot, uint32_t& ioff, uint32_t& bv)
+{
+    const uint8_t* in = sc.instances + size_t(id) * 160;
+    const float* T = reinterpret_cast<const float*>(in + 32);            // transform rows
+    rot = m3{{V3(T[0], T[1], T[2]), V3(T[4], T[5], T[6]), V3(T[8], T[9], T[10])}};
+    ioff = reinterpret_cast<const uint32_t*>(in)[4];
+    bv = reinterpret_cast<const uint32_t*>(in)[5];
 }
 
 struct HitInfo {
@@ -368,8 +567,8 @@ PTG_D float4 ld4(const float* base, uint32_t i) { return reinterpret_cast<const 
 // hit of the ray (origin, dir) into a hit_info.
 // KIND: 0 = either, 1 = the caller knows the ray hit, 2 = it knows it missed
 // (lets the wavefront kernels compile only the branch they run).
-template<bool COUNT, int KIND = 0>
-PTG_D HitInfo hit_info(const DevScene& sc, const Light& L, f3 origin, f3 dir, const Hit& h, Counters& cnt)
+template<bool COUNT, int KIND = 0, class SC>
+PTG_D HitInfo hit_info(const SC& sc, const Light& L, f3 origin, f3 dir, const Hit& h, Counters& cnt)
 {
     HitInfo hi;
     hi.thit = h.thit;
@@ -388,10 +587,9 @@ PTG_D HitInfo hit_info(const DevScene& sc, const Light& L, f3 origin, f3 dir, co
     }
     if(COUNT) cnt.shades++;
     hi.pos = origin + dir * h.thit;
-    const float4* sp = reinterpret_cast<const float4*>(sc.inst_shade + h.instance_id);
-    const float4 s0 = sp[0], s1 = sp[1], s2 = sp[2];
-    const m3 rot{{V3(s0.x, s0.y, s0.z), V3(s0.w, s1.x, s1.y), V3(s1.z, s1.w, s2.x)}};
-    const uint32_t ioff = __float_as_uint(s2.y), bv = __float_as_uint(s2.z);
+    m3 rot;
+    uint32_t ioff, bv;
+    shade_instance(sc, h.instance_id, rot, ioff, bv);
     const uint32_t tri = ioff + h.primitive_id * 3;
     const uint32_t i0 = sc.indices[tri] + bv, i1 = sc.indices[tri + 1] + bv, i2 = sc.indices[tri + 2] + bv;
     const f3 n0 = ld3(sc.normal, i0), n1 = ld3(sc.normal, i1), n2 = ld3(sc.normal, i2);
@@ -414,13 +612,13 @@ PTG_D HitInfo hit_info(const DevScene& sc, const Light& L, f3 origin, f3 dir, co
 }
 
 // trace_ray (path_tracer.hh:340-412)
-template<bool COUNT>
-PTG_D HitInfo trace_ray(const DevScene& sc, uint32_t tc, uint32_t to, const Light& L, f3 origin, f3 dir, float tmin,
+template<bool COUNT, class SC>
+PTG_D HitInfo trace_ray(const SC& sc, uint32_t tc, uint32_t to, const Light& L, f3 origin, f3 dir, float tmin,
                         Counters& cnt)
 {
     Hit h;
     trace<false, COUNT>(sc, tc, to, origin, dir, tmin, 1e9f, h, cnt);
-    return hit_info<COUNT>(sc, L, origin, dir, h, cnt);
+    return hit_info<COUNT, 0>(sc, L, origin, dir, h, cnt);
 }
 
 // ---- samplers (path_tracer.hh:12-83) ----
@@ -782,8 +980,8 @@ PTG_D f3 nee_finish(const NeeCandidate& c, f3 pos)
     return color / c.mis_pdf;
 }
 
-template<bool COUNT>
-PTG_D f3 nee_branch(const DevScene& sc, uint32_t tc, uint32_t to, u4& seed, const Light& L, const HitInfo& info,
+template<bool COUNT, class SC>
+PTG_D f3 nee_branch(const SC& sc, uint32_t tc, uint32_t to, u4& seed, const Light& L, const HitInfo& info,
                     const Material& M, f3 tview, Counters& cnt)
 {
     NeeCandidate c;
@@ -802,7 +1000,8 @@ PTG_D f3 rd_f3(const uint8_t* p, uint32_t off)
 }
 
 // subframes[sample_index / SAMPLES_PER_MOTION_BLUR_STEP] (path_tracer.hh:655-657)
-PTG_D const uint8_t* subframe_of(const DevScene& sc, int32_t sample_index)
+template<class SC>
+PTG_D const uint8_t* subframe_of(const SC& sc, int32_t sample_index)
 {
     const uint32_t sub = sample_index < 0 ? 0u : (uint32_t)sample_index / sc.blur_step;
     return sc.subframes + size_t(sub) * SF_STRIDE;
@@ -817,7 +1016,8 @@ PTG_D Light light_of(const uint8_t* sf)
 }
 
 // Seed initialisation, film jitter and get_camera_ray (path_tracer.hh:659-671, :429-450).
-PTG_D void camera_ray(const DevScene& sc, const uint8_t* sf, uint32_t px, uint32_t py, int32_t sample_index, u4& seed,
+template<class SC>
+PTG_D void camera_ray(const SC& sc, const uint8_t* sf, uint32_t px, uint32_t py, int32_t sample_index, u4& seed,
                       f3& ray_o, f3& ray_dir)
 {
     seed = u4{px, py, (uint32_t)sample_index, sc.student_id};
@@ -880,8 +1080,8 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
 // path_trace_pixel (path_tracer.hh:637-741) as one device function (used by
 // the per-sample entry point; the frame renderer runs the same steps as a
 // wavefront pipeline, csrc/device/wavefront.h).
-template<bool COUNT>
-PTG_D f3 path_trace_sample(const DevScene& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
+template<bool COUNT, class SC>
+PTG_D f3 path_trace_sample(const SC& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
 {
     const uint8_t* sf = subframe_of(sc, sample_index);
     const uint32_t tc = rd_u(sf, SF_TLAS), to = rd_u(sf, SF_TLAS + 4);

@@ -349,18 +349,26 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                     if(v < end && t < n)
                     {
                         q = ANY ? list[t] : t;
-#if PTG_NT_STATE
-                        // path state streams once through the caches: non-temporal, so it
-                        // does not evict BVH records from L2 / the Infinity Cache
-                        const uint4 m = nt_load(S.meta + q);
-                        w.init(sc, m.z, m.w, xyz(nt_load(S.ray_o + q)), ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)),
-                               tmin, tmax);
-#else
-                        const uint4 m = S.meta[q];
-                        w.init(sc, m.z, m.w, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
+#if PTG_DEBUG
+                        // the NEE list names positions of this round's path queue
+                        const bool bad = ANY && q >= counts[2 * round];
+                        if(bad && sc.debug) atomicAdd(sc.debug + kDebugQueue, 1u);
+                        if(!bad)
 #endif
-                        active = true;
-                        if(COUNT) cnt.queries++;
+                        {
+#if PTG_NT_STATE
+                            // path state streams once through the caches: non-temporal, so it
+                            // does not evict BVH records from L2 / the Infinity Cache
+                            const uint4 m = nt_load(S.meta + q);
+                            w.init(sc, m.z, m.w, xyz(nt_load(S.ray_o + q)),
+                                   ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)), tmin, tmax);
+#else
+                            const uint4 m = S.meta[q];
+                            w.init(sc, m.z, m.w, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
+#endif
+                            active = true;
+                            if(COUNT) cnt.queries++;
+                        }
                     }
                 }
                 cursor = min(end, cursor + nidle);
@@ -517,7 +525,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         const uint32_t i = base + threadIdx.x;
         bool cont = false, nee = false;
         PathRec p;
+#if PTG_DEBUG
+        const bool bad_q = i < n && hit_list[i] >= counts[2 * round];
+        if(bad_q && sc.debug) atomicAdd(sc.debug + kDebugList, 1u);
+        if(i < n && !bad_q)
+#else
         if(i < n)
+#endif
         {
             Hit h;
             bool occluded;
@@ -572,6 +586,13 @@ __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, Pat
     Counters cnt;
     for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     {
+#if PTG_DEBUG
+        if(sky_list[i] >= lcounts[0] + lcounts[1])   // positions of this round's queue (hits + sky)
+        {
+            if(sc.debug) atomicAdd(sc.debug + kDebugList, 1u);
+            continue;
+        }
+#endif
         PathRec p;
         Hit h;
         bool occluded;
@@ -747,6 +768,7 @@ struct ptg_context {
     bool frame_ready = false;
     // render workspace
     DevBuf samples, acc, tmp_a, tmp_b, tmp_c, counters;
+    DevBuf debug;                          // PTG_DEBUG builds: kDebugSlots violation counters
     uint64_t last_counters[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // k_trace launch timing (HIP events on the launch stream)
     bool timing = false;
@@ -757,10 +779,14 @@ struct ptg_context {
     int pipeline = 0;
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
-    uint32_t walk_xcds[2] = {1, 1};
-    uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state, padded to cap residency        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
-    uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM (PTG_HBM_PCT)
-    uint32_t chunk_log2 = 28;              // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2)   // resident blocks of k_wf_walk<closest/any>
+    uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
+    uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state, padded to cap residency
+    uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (PTG_HBM_PCT)
+    // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2).  2^27
+    // paths x 392 B = 53 GB per pipeline, ~37% of an MI355X's HBM for the two
+    // pipelines together, so a default render leaves most of the GPU to other
+    // tenants; 2^28 (73%) is 1-3% faster on a GPU the renderer owns alone.
+    uint32_t chunk_log2 = 27;
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
     // second stream for the sky kernels + the events that order it with `stream`
@@ -827,6 +853,10 @@ struct ptg_context {
         s.student_id = cfg ? cfg->student_id : 0;
         s.blur_step = cfg ? cfg->samples_per_motion_blur_step : 8;
         s.subframe_count = uint32_t(subframe_count);
+        s.trav_count = uint32_t(std::min<size_t>(trav.bytes / sizeof(TravRec), 8 * (first_frame_node + frame_node_count)));
+        s.tri_count = uint32_t(index_count / 3);
+        s.inst_count = uint32_t(instance_count);
+        s.debug = PTG_DEBUG ? debug.as<uint32_t>() : nullptr;
         return s;
     }
 };
@@ -1124,6 +1154,22 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipEventRecord(ctx->ev_acc_end, ctx->acc_stream));
         PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_acc_end, 0));
     }
+#if PTG_DEBUG
+    {
+        uint32_t dbg[kDebugSlots];
+        PTG_HIP(hipStreamSynchronize(ctx->stream));
+        PTG_HIP(hipMemcpy(dbg, ctx->debug.p, sizeof(dbg), hipMemcpyDeviceToHost));
+        std::string bad;
+        static const char* names[kDebugSlots] = {"node record", "triangle", "instance", "NEE list", "shade list", "", "", ""};
+        for(uint32_t k = 0; k < kDebugSlots; ++k)
+            if(dbg[k]) bad += std::string(bad.empty() ? "" : ", ") + names[k] + " index out of range x" + std::to_string(dbg[k]);
+        if(!bad.empty())
+        {
+            PTG_HIP(hipMemset(ctx->debug.p, 0, sizeof(dbg)));
+            return fail(PTG_E_RANGE, "PTG_DEBUG: " + bad);
+        }
+    }
+#endif
     if(ctx->counting)
     {
         unsigned long long host[K_KINDS * 8];
@@ -1253,6 +1299,10 @@ int ptg_context_create(int device, ptg_context** out)
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
+#if PTG_DEBUG
+    PTG_HIP(ctx->debug.reserve(kDebugSlots * sizeof(uint32_t)));
+    PTG_HIP(hipMemset(ctx->debug.p, 0, kDebugSlots * sizeof(uint32_t)));
+#endif
     if(getenv("PTG_NO_OVERLAP") == nullptr)
     {
         PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
@@ -1364,11 +1414,16 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
         }
     }
 
-    // validate handles, pack instances, collect BLAS / mesh packing jobs
+    // validate handles, pack instances, collect BLAS / mesh packing jobs.  The
+    // BLASes and meshes this call packs are collected locally and join the
+    // context's packed sets only after every check and every packing launch
+    // succeeded: an upload that fails half-way never leaves the sets claiming
+    // records that were not written.
     std::vector<InstTrav> it(instance_count);
     std::vector<InstShade> is(instance_count);
     std::vector<BvhJob> blas_jobs;
     std::vector<MeshJob> mesh_jobs;
+    std::unordered_set<uint32_t> new_bvh, new_mesh;
     for(size_t i = 0; i < instance_count; ++i)
     {
         const ptg_tlas_instance& in = instances[i];
@@ -1393,10 +1448,10 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
         is[i].index_offset = in.m.index_offset;
         is[i].base_vertex_offset = in.m.base_vertex_offset;
         std::fill(is[i].pad, is[i].pad + 5, 0u);
-        if(ctx->packed_bvh.insert(in.blas.node_offset).second)
+        if(!ctx->packed_bvh.count(in.blas.node_offset) && new_bvh.insert(in.blas.node_offset).second)
             blas_jobs.push_back(BvhJob{in.blas.node_offset, in.blas.node_offset * 8, in.blas.node_count,
                                        in.blas.node_offset * 8});
-        if(ctx->packed_mesh.insert(in.m.index_offset).second)
+        if(!ctx->packed_mesh.count(in.m.index_offset) && new_mesh.insert(in.m.index_offset).second)
             mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
     }
     std::vector<BvhJob> tlas_jobs;
@@ -1450,6 +1505,8 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
         PTG_HIP(hipGetLastError());
     }
     PTG_HIP(hipStreamSynchronize(s));
+    ctx->packed_bvh.insert(new_bvh.begin(), new_bvh.end());
+    ctx->packed_mesh.insert(new_mesh.begin(), new_mesh.end());
     ctx->first_frame_node = first_node;
     ctx->frame_node_count = frame_node_count;
     ctx->subframe_count = subframe_count;
@@ -1624,6 +1681,47 @@ int ptg_last_kernel_times(ptg_context* ctx, double ms[8], uint32_t launches[8])
         PTG_HIP(hipEventElapsedTime(&t, ctx->ev_start[i], ctx->ev_stop[i]));
         ms[ctx->ev_kind[i]] += t;
         launches[ctx->ev_kind[i]] += 1;
+    }
+    ctx->ev_used = 0;
+    return PTG_OK;
+}
+
+int ptg_last_kernel_busy(ptg_context* ctx, double busy_ms[8], double ms[8], uint32_t launches[8])
+{
+    if(int r = bind(ctx)) return r;
+    if(!busy_ms || !ms || !launches) return fail(PTG_E_INVALID, "ptg_last_kernel_busy: bad arguments");
+    struct Iv { int kind; double s, e; };
+    std::vector<Iv> iv;
+    iv.reserve(ctx->ev_used);
+    for(size_t i = 0; i < ctx->ev_used; ++i)
+    {
+        PTG_HIP(hipEventSynchronize(ctx->ev_stop[i]));
+        float s = 0, e = 0;
+        // every launch's interval on one time axis: relative to the first recorded start
+        PTG_HIP(hipEventElapsedTime(&s, ctx->ev_start[0], ctx->ev_start[i]));
+        PTG_HIP(hipEventElapsedTime(&e, ctx->ev_start[0], ctx->ev_stop[i]));
+        iv.push_back(Iv{ctx->ev_kind[i], double(s), double(e)});
+    }
+    std::sort(iv.begin(), iv.end(), [](const Iv& a, const Iv& b) { return a.s < b.s; });
+    for(int k = 0; k < 8; ++k)
+    {
+        busy_ms[k] = ms[k] = 0;
+        launches[k] = 0;
+        double cs = 0, ce = -1;   // current merged interval of kind k
+        for(const Iv& v: iv)
+        {
+            if(v.kind != k) continue;
+            ms[k] += v.e - v.s;
+            launches[k] += 1;
+            if(v.s > ce)
+            {
+                if(ce > cs) busy_ms[k] += ce - cs;
+                cs = v.s;
+                ce = v.e;
+            }
+            else ce = std::max(ce, v.e);
+        }
+        if(ce > cs) busy_ms[k] += ce - cs;
     }
     ctx->ev_used = 0;
     return PTG_OK;

@@ -95,30 +95,48 @@ def assemble_numpy(shard: TileShard, gathered, image):
 
 
 def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None):
-    """Render this rank's tiles and gather them into `image` on rank 0 (RCCL)."""
+    """Render this rank's tiles and gather them into `image` on rank 0.
+
+    `renderer` provides render_tiles / scatter_tiles (GpuRenderer, or any
+    object with the same two methods).  Everything - the render, the gather
+    and the scatter - is issued on `stream` (a torch.cuda.Stream; default:
+    the current stream), which must be the stream the renderer launches on:
+    RCCL then orders the collective after the tiles were written, and the
+    scatter after the collective, with no host synchronisation.  Whenever a
+    process group is initialised the collective runs, at world size 1 too;
+    only a process with no group at all takes the local path.  Over gloo
+    (CPU groups: tests, rehearsals) the tiles go through host memory.
+    """
+    import contextlib
+
     import torch
     import torch.distributed as dist
     dev = image.device
     per_tile = shard.tile_w * shard.tile_h
-    buf = torch.zeros((shard.max_count * per_tile, 4), dtype=torch.uint8, device=dev)
-    if shard.count:
-        renderer.render_tiles(cfg, shard.tile_w, shard.tile_h, shard.first, shard.stride, shard.count,
-                              out_bgra=buf[:shard.count * per_tile])
-    if shard.world == 1:
-        parts = [buf]
-    elif dist.get_backend() == "gloo":   # CPU process groups (tests, rehearsals): gather through host memory
-        host = buf.cpu()
-        hparts = [torch.empty_like(host) for _ in range(shard.world)] if shard.rank == 0 else None
-        dist.gather(host, hparts, dst=0)
-        parts = [p.to(dev) for p in hparts] if shard.rank == 0 else None
-    else:
-        parts = [torch.empty_like(buf) for _ in range(shard.world)] if shard.rank == 0 else None
-        dist.gather(buf, parts, dst=0)
-    if shard.rank == 0:
-        for r, part in enumerate(parts):
-            n = shard.count_for(r)
-            if n:
-                renderer.scatter_tiles(cfg, shard.tile_w, shard.tile_h, r, shard.world, n, part, image)
+    ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
+    with ctx:
+        buf = torch.zeros((shard.max_count * per_tile, 4), dtype=torch.uint8, device=dev)
+        if shard.count:
+            renderer.render_tiles(cfg, shard.tile_w, shard.tile_h, shard.first, shard.stride, shard.count,
+                                  out_bgra=buf[:shard.count * per_tile])
+        grouped = dist.is_available() and dist.is_initialized()
+        if not grouped:
+            if shard.world != 1:
+                raise RuntimeError("render_and_gather: world size %d but no process group" % shard.world)
+            parts = [buf]
+        elif dist.get_backend() == "gloo":   # CPU process groups: gather through host memory
+            host = buf.cpu()
+            hparts = [torch.empty_like(host) for _ in range(shard.world)] if shard.rank == 0 else None
+            dist.gather(host, hparts, dst=0)
+            parts = [p.to(dev) for p in hparts] if shard.rank == 0 else None
+        else:                                # RCCL over xGMI: one gather of the uchar4 tiles to rank 0
+            parts = [torch.empty_like(buf) for _ in range(shard.world)] if shard.rank == 0 else None
+            dist.gather(buf, parts, dst=0)
+        if shard.rank == 0:
+            for r, part in enumerate(parts):
+                n = shard.count_for(r)
+                if n:
+                    renderer.scatter_tiles(cfg, shard.tile_w, shard.tile_h, r, shard.world, n, part, image)
     return image
 
 

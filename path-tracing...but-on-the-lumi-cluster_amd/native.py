@@ -108,6 +108,7 @@ def lib():
         "ptg_timing_enable": (I, [P, I]),
         "ptg_last_timing": (I, [P, C.POINTER(C.c_double), C.POINTER(U32)]),
         "ptg_last_kernel_times": (I, [P, P, P]),
+        "ptg_last_kernel_busy": (I, [P, P, P, P]),
         "ptg_last_kernel_counters": (I, [P, P]),
         "ptg_set_pipeline": (I, [P, I]),
         "ptg_set_concurrency": (I, [P, I]),

@@ -57,8 +57,9 @@ class GpuRenderer:
                 "ptg_upload_from_scene")
         self.scene_uploaded = True
 
-    def upload_arrays(self, arrays: dict, include_static=True):
-        """Upload reference-layout numpy arrays (the keys of Scene.view())."""
+    def upload_arrays(self, arrays: dict, include_static=True, include_frame=True):
+        """Upload reference-layout numpy arrays (the keys of Scene.view()):
+        ptg_upload_scene (include_static) and/or ptg_upload_frame (include_frame)."""
         L = N.lib()
         a = {k: (np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v) for k, v in arrays.items()}
         sn = int(a["static_node_count"])
@@ -67,6 +68,9 @@ class GpuRenderer:
                                        a["indices"].ctypes.data, a["indices"].size, a["pos"].ctypes.data,
                                        a["normal"].ctypes.data, a["albedo"].ctypes.data, a["material"].ctypes.data,
                                        a["pos"].shape[0]), "ptg_upload_scene")
+        if not include_frame:
+            self.scene_uploaded = self.scene_uploaded or include_static
+            return
         nodes = a["nodes"][sn:]
         links = a["links"][8 * sn:]
         N.check(L.ptg_upload_frame(self._ctx, a["subframes"].ctypes.data, a["subframes"].size,
@@ -152,6 +156,17 @@ class GpuRenderer:
         n = np.zeros(8, np.uint32)
         N.check(N.lib().ptg_last_kernel_times(self._ctx, ms.ctypes.data, n.ctypes.data), "ptg_last_kernel_times")
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KINDS)}
+
+    def kernel_busy(self):
+        """{kind: (busy ms, summed ms, launches)}: busy = the union of the
+        recorded launches' device intervals (overlapping launches of one kind
+        counted once); waits for them and clears the record."""
+        busy = np.zeros(8, np.float64)
+        ms = np.zeros(8, np.float64)
+        n = np.zeros(8, np.uint32)
+        N.check(N.lib().ptg_last_kernel_busy(self._ctx, busy.ctypes.data, ms.ctypes.data, n.ctypes.data),
+                "ptg_last_kernel_busy")
+        return {k: (float(busy[i]), float(ms[i]), int(n[i])) for i, k in enumerate(self.KINDS)}
 
     def kernel_counters(self):
         """{kind: counters[8]} of the last render call (counting enabled)."""

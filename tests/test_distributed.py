@@ -1,5 +1,6 @@
-"""Multi-GPU sharding logic on CPU: tile partition, frame partition and the
-framebuffer gather over a real world_size-2 process group (gloo)."""
+"""Multi-GPU sharding logic on CPU: tile partition, frame partition, and the
+product's render_and_gather (distributed.py) over real world-size 2 and 3
+process groups (gloo) with a stub renderer in place of the GPU."""
 import os
 import socket
 
@@ -41,32 +42,60 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class StubRenderer:
+    """Stands in for GpuRenderer on CPU: render_tiles writes each pixel slot's
+    own coordinates (and the rank), scatter_tiles places a dense tile buffer
+    into the image exactly as ptg_scatter_tiles does (through TileShard.pixels)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.calls = []
+
+    def render_tiles(self, cfg, tw, th, first, stride, count, out_bgra=None):
+        self.calls.append(("render_tiles", first, stride, count))
+        sh = D.TileShard(cfg, tw, th, first, stride)
+        x, y = sh.pixels()
+        n = count * tw * th
+        buf = out_bgra.view(-1, 4)
+        assert buf.shape[0] == n == len(x)
+        buf[:, 0] = torch.from_numpy(np.where(x >= 0, x % 251, 0).astype(np.uint8))
+        buf[:, 1] = torch.from_numpy(np.where(y >= 0, y % 241, 0).astype(np.uint8))
+        buf[:, 2] = self.rank
+        buf[:, 3] = 255
+        return out_bgra, None
+
+    def scatter_tiles(self, cfg, tw, th, first, stride, count, tiles_bgra, image_bgra):
+        self.calls.append(("scatter_tiles", first, stride, count))
+        sh = D.TileShard(cfg, tw, th, first, stride)
+        x, y = sh.pixels()
+        ok = x >= 0
+        t = tiles_bgra.view(-1, 4)[:len(x)].numpy()
+        img = image_bgra.numpy()
+        img[y[ok], x[ok]] = t[ok]
+
+
 def _worker(rank, world, port, w, h, tw, th, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = N.RenderConfig.make(w, h, 8)
     shard = D.TileShard(cfg, tw, th, rank, world)
-    x, y = shard.pixels()
-    # stand-in for ptg_render_tiles: each pixel slot holds its own coordinates
-    buf = np.zeros((shard.max_count * tw * th, 4), np.uint8)
-    n = len(x)
-    buf[:n, 0] = np.where(x >= 0, x % 251, 0)
-    buf[:n, 1] = np.where(y >= 0, y % 241, 0)
-    buf[:n, 2] = rank
-    buf[:n, 3] = 255
-    t = torch.from_numpy(buf)
-    parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-    dist.gather(t, parts, dst=0)
+    image = torch.zeros((h, w, 4), dtype=torch.uint8)
+    stub = StubRenderer(rank)
+    D.render_and_gather(stub, cfg, shard, image)          # the product function, collective included
     if rank == 0:
-        img = np.zeros((h, w, 4), np.uint8)
-        D.assemble_numpy(shard, [p.numpy() for p in parts], img)
-        np.save(out, img)
+        np.save(out, image.numpy())
+        # rank 0 rendered its own tiles and scattered every rank's part
+        assert stub.calls[0] == ("render_tiles", 0, world, shard.count)
+        assert [c[1] for c in stub.calls[1:]] == list(range(world))
+    else:
+        assert stub.calls == [("render_tiles", rank, world, shard.count)]
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gather_assembles_framebuffer_gloo(tmp_path):
-    w, h, tw, th, world = 100, 60, 16, 8, 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_assembles_framebuffer_gloo(tmp_path, world):
+    w, h, tw, th = 100, 60, 16, 8
     out = str(tmp_path / "img.npy")
     mp.spawn(_worker, args=(world, _free_port(), w, h, tw, th, out), nprocs=world, join=True)
     img = np.load(out)
@@ -76,3 +105,14 @@ def test_gather_assembles_framebuffer_gloo(tmp_path):
     owner = ((yy // th) * tiles_x + xx // tw) % world
     assert np.array_equal(img[..., 2], owner)
     assert (img[..., 3] == 255).all()
+
+
+def test_render_and_gather_without_group_is_local():
+    cfg = N.RenderConfig.make(40, 20, 8)
+    shard = D.TileShard(cfg, 16, 8, 0, 1)
+    image = torch.zeros((20, 40, 4), dtype=torch.uint8)
+    D.render_and_gather(StubRenderer(0), cfg, shard, image)
+    yy, xx = np.mgrid[0:20, 0:40]
+    assert np.array_equal(image[..., 0].numpy(), xx % 251) and np.array_equal(image[..., 1].numpy(), yy % 241)
+    with pytest.raises(RuntimeError, match="no process group"):
+        D.render_and_gather(StubRenderer(0), cfg, D.TileShard(cfg, 16, 8, 0, 2), image)

@@ -40,3 +40,63 @@ def test_tiles_assemble_to_single_gpu_frame(gpu, assets_dir, tw, th, world):
     parts = [np.concatenate([p, np.zeros((pad - len(p), 4), np.uint8)]) for p in parts]
     D.assemble_numpy(D.TileShard(cfg, tw, th, 0, world), parts, host_img)
     assert np.array_equal(host_img, full)
+
+
+def test_metric_config_eight_shards_match_frame(gpu, assets_dir):
+    """BASELINE configs[2]: the metric frame (frame 0, 1280x720, 1024 spp) cut
+    into interleaved 32x16 tiles for 8 ranks, each shard rendered through
+    ptg_render_tiles and scattered: the assembled frame equals the single-GPU
+    render byte for byte, and so does the averaged radiance of every shard."""
+    import torch
+    s = scene_for(assets_dir, 1280, 720, 1024, frame=0)
+    gpu.upload_arrays(arrays_copy(s))
+    cfg = s.cfg
+    full, acc_full = gpu.render(cfg, want_accum=True)
+    img = torch.zeros((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda:0")
+    acc_full = acc_full.cpu().numpy()
+    for r in range(8):
+        sh = D.TileShard(cfg, 32, 16, r, 8)
+        n = sh.count * 32 * 16
+        acc_t = torch.empty((n, 4), dtype=torch.float32, device="cuda:0")
+        tiles, _ = gpu.render_tiles(cfg, 32, 16, sh.first, sh.stride, sh.count, out_accum=acc_t)
+        gpu.scatter_tiles(cfg, 32, 16, sh.first, sh.stride, sh.count, tiles, img)
+        gpu.synchronize()
+        x, y = sh.pixels()
+        ok = x >= 0
+        got = acc_t.cpu().numpy()[ok, :3].view(np.uint32)
+        assert np.array_equal(got, acc_full[y[ok], x[ok], :3].view(np.uint32)), r
+    gpu.synchronize()
+    assert np.array_equal(img.cpu().numpy(), full.cpu().numpy())
+
+
+def test_render_and_gather_over_rccl(gpu, assets_dir):
+    """The product's render_and_gather with its collective executed over RCCL
+    (torch.distributed 'nccl'): a world-size-1 process group on this GPU, so
+    dist.gather runs on the device stream exactly as on 8 GPUs (RCCL cannot
+    put two ranks on one GPU).  The gathered, scattered frame equals the
+    single-GPU render."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    s = scene_for(assets_dir, 640, 360, 32, frame=450)
+    gpu.upload_arrays(arrays_copy(s))
+    cfg = s.cfg
+    full, _ = gpu.render(cfg)
+    gpu.synchronize()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    stream = torch.cuda.Stream()
+    gpu.set_stream(stream)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        img = torch.zeros((cfg.height, cfg.width, 4), dtype=torch.uint8, device="cuda:0")
+        D.render_and_gather(gpu, cfg, D.TileShard(cfg, 32, 16, 0, 1), img, stream=stream)
+        stream.synchronize()
+        assert np.array_equal(img.cpu().numpy(), full.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+        gpu.set_stream(torch.cuda.default_stream())

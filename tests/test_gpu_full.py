@@ -176,3 +176,46 @@ def test_baseline_configs_spot_rects_bit_exact(gpu, assets_dir, w, h, spp, frame
         acc_o, bgra_o = orc.render_rect(x0, y0, rw, rh)
         assert np.array_equal(_bits(acc[y0:y0 + rh, x0:x0 + rw, :3]), _bits(acc_o[..., :3])), (x0, y0)
         assert np.array_equal(bgra[y0:y0 + rh, x0:x0 + rw], bgra_o), (x0, y0)
+
+
+def test_failed_frame_upload_leaves_no_stale_records(gpu, assets_dir):
+    """a frame upload that fails after its instance loop must not
+    leave the packed-BLAS/mesh sets claiming records it never wrote.  Sequence:
+    upload_scene (clears the sets), a frame whose TLAS names a missing instance
+    (rejected after every instance was checked), then the good frame without
+    the static part - which must repack and render bit-exact."""
+    s = scene_for(assets_dir, 320, 180, 16, frame=450)
+    arr = arrays_copy(s)
+    gpu.upload_arrays(arr, include_static=True, include_frame=False)
+    bad = dict(arr)
+    bad["instances"] = arr["instances"][: len(arr["instances"]) // 2]
+    with pytest.raises(N.PtgError, match=r"\(-6\).*TLAS leaf"):
+        gpu.upload_arrays(bad, include_static=False)
+    gpu.upload_arrays(arr, include_static=False)
+    rect = (150, 80, 6, 4)
+    _, acc = gpu.render(s.cfg, rect=rect, want_accum=True)
+    gpu.synchronize()
+    acc_o, _ = Oracle(arr, s.cfg).render_rect(*rect)
+    assert np.array_equal(_bits(acc.cpu().numpy()[..., :3]), _bits(acc_o[..., :3]))
+
+
+@pytest.mark.timeout(600)
+def test_config4_full_4096spp_spot_rects_bit_exact(gpu, assets_dir):
+    """BASELINE configs[4] at its full size: 3840x2160, 4096 spp (512
+    subframes), frame 690 with the dragon and the buddha in view - the render
+    the bench times (~70 s), spot rectangles bit-exact against the oracle."""
+    w, h, spp, frame = 3840, 2160, 4096, 690
+    s = scene_for(assets_dir, w, h, spp, frame=frame)
+    arr = arrays_copy(s)
+    gpu.upload_arrays(arr)
+    bgra, acc = gpu.render(s.cfg, want_accum=True)
+    gpu.synchronize()
+    rects = [(0, 0, 2, 2), (1900, 1000, 4, 4), (3000, 1500, 4, 2), (2400, 1200, 2, 4), (3836, 2158, 4, 2)]
+    acc_h = acc.cpu().numpy()
+    bgra_h = bgra.cpu().numpy()
+    orc = Oracle(arr, s.cfg)
+    for x0, y0, rw, rh in rects:
+        acc_o, bgra_o = orc.render_rect(x0, y0, rw, rh)
+        assert np.array_equal(_bits(acc_h[y0:y0 + rh, x0:x0 + rw, :3]), _bits(acc_o[..., :3])), (x0, y0)
+        assert np.array_equal(bgra_h[y0:y0 + rh, x0:x0 + rw], bgra_o), (x0, y0)
+    assert np.isfinite(acc_h).all() and (bgra_h[..., 3] == 255).all()
