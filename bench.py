@@ -5,31 +5,41 @@ tonemap_pixel under baseline_render, on MI355X.
 Workload (the configuration BASELINE.json's metric is quoted on, "1280x720
 1024spp"; configs[1] is the same frame at 256 spp): frame 0 of the reference
 animation, 1280x720, 1024 samples per pixel, MAX_BOUNCES = 4 (the shipped
-TESTING preset), the reference scene (reference OBJ assets + committed substitutes for
-the three missing meshes).  One step = one baseline_render of the frame on the GPU (+ the RCCL
-framebuffer gather in --shard tiles mode) with the scene and the frame's
-TLAS/instances/subframes already resident in HBM: `value`.  A second timed
-loop runs what main.cc does per frame - setup_animation_frame (host C++) +
-H2D upload of the frame data + render - issued asynchronously so the host
-setup of step k+1 overlaps the render of step k (ptg_upload_frame waits for
-the previous render before overwriting the frame buffers); it is reported
-as "with_frame_setup" (PCIe-inclusive, never `value`).
+TESTING preset), the reference scene (reference OBJ assets + committed
+substitutes for the three missing meshes).  One step = one baseline_render of
+the frame on the GPU (+ the RCCL framebuffer gather in --shard tiles mode)
+with the scene and the frame's TLAS/instances/subframes already resident in
+HBM: `value`.
+
+Beside `value` the line carries (rank 0):
+  with_frame_setup  what main.cc does per frame - setup_animation_frame (host
+                    C++) + H2D upload + render, pipelined (PCIe-inclusive,
+                    never `value`);
+  heavy_frame       the same metric on frame 450 (buddha close-up, ~7x the
+                    per-sample work of frame 0; SURVEY 8(d) config 2's heavy
+                    companion);
+  animation         frames spread evenly over the 1800-frame animation, each
+                    set up, uploaded, rendered and written as a BMP
+                    asynchronously (main.cc:78-101, bmp.cc) - frames/min and
+                    the average Msamples/s; spot rectangles of every frame's
+                    radiance are saved for the oracle check
+                    (tests/test_animation_spots.py);
+  roofline          the dominant kernel, k_wf_walk<closest> (the closest-hit
+                    BVH walk), against ceilings measured per level of the
+                    memory hierarchy (DESIGN.md section 5);
+  cpu_baseline      the reference's own baseline_render built from its sources,
+                    timed on this host's cores (bounded samples).
 
 Multi-GPU: one process per GPU (torch.distributed.run).  --shard frames
 (default): rank r renders frame (frame + r) - weak scaling, no collective on
 the data path (BASELINE config 4 style).  --shard tiles: one frame split into
 interleaved 32x16 tiles, rank 0 gathers the BGRA tiles over RCCL and
 assembles the framebuffer - strong scaling (config 3 style).
-
-Prints ONE JSON line (rank 0) with the driver contract fields plus
-"roofline" (the dominant kernel k_wf_walk<closest>: its algorithmic bytes
-from the deterministic work counters / its device time from HIP events on the
-launch stream, vs 8 TB/s HBM) and "cpu_baseline" (the reference's own baseline_render built
-from its sources, timed on this host's cores on a bounded sample).
 """
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -39,23 +49,22 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROFILES = os.path.join(ROOT, "profiles")
+CEILINGS = os.path.join(PROFILES, "r02_probe", "ceilings.json")
 
 
-def pmc_traffic(kind, workload, ms_per_launch):
-    """HBM-side bytes per launch of `kind` from committed rocprofv3 PMC passes
-    of this same workload and code (tools/profile_gpu.sh + summarize_prof.py):
-    FETCH_SIZE x 1 KiB x 2 (gfx950 correction) + WRITE_SIZE x 1 KiB.  A
-    profile counts only if its kernel-trace average launch time agrees with the
-    live measurement within 15% (a profile of older code or another chunking
-    is not used), the newest (by profile name) when several do; None when
-    none does."""
+def _natural(path):   # r01_wavefront11 after r01_wavefront9
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
+
+
+def pmc_profile(kind, workload, ms_per_launch):
+    """Per-launch PMC counters of `kind` from the newest committed rocprofv3
+    profile of this workload (tools/profile_gpu.sh + summarize_prof.py) whose
+    kernel-trace average launch time agrees with `ms_per_launch` (the same
+    kernel measured alone in this run) within 15%: a profile of other code or
+    another chunking is never used.  Returns (counters dict, path) or (None, None)."""
     import glob
-    import re
-
-    def natural(path):   # r01_wavefront11 after r01_wavefront9
-        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
-    best = None
-    for f in sorted(glob.glob(os.path.join(PROFILES, "*", "pmc_summary.json")), key=natural):
+    best = (None, None)
+    for f in sorted(glob.glob(os.path.join(PROFILES, "*", "pmc_summary.json")), key=_natural):
         try:
             with open(f) as fh:
                 prof = json.load(fh)
@@ -64,45 +73,154 @@ def pmc_traffic(kind, workload, ms_per_launch):
                 continue
             if abs(ent["trace_avg_ms"] - ms_per_launch) > 0.15 * ms_per_launch:
                 continue
-            best = (int(ent["derived"]["hbm_side_bytes"]), os.path.relpath(f, ROOT))   # the newest that qualifies
+            best = (ent, os.path.relpath(f, ROOT))
         except (OSError, KeyError, ValueError, TypeError):
             continue
-    return best if best else (None, None)
+    return best
 
 
 def algorithmic_bytes(c):
     """B = 32 N_node + 60 N_tri + 88 N_enter + 156 N_hit + 160 per sample.
 
-    32 B TravRec per node visit (24 B box + 8 B link in the reference layout),
-    60 B per triangle test (3 x u32 index + 3 x 16 B position), 88 B per BLAS
-    entry (blas + mesh + inv_transform), 156 B per closest-hit shade (3 x u32 +
-    9 x 16 B vertex attributes), 160 B subframe per sample."""
+    32 B per node visit (24 B box + 8 B link in the reference layout), 60 B per
+    triangle test (3 x u32 index + 3 x 16 B position), 88 B per BLAS entry
+    (blas + mesh + inv_transform), 156 B per closest-hit shade (3 x u32 + 9 x
+    16 B vertex attributes), 160 B subframe per sample."""
     samples, visits, tris, enters, queries, shades = [int(x) for x in c[:6]]
     return 32 * visits + 60 * tris + 88 * enters + 156 * shades + 160 * samples
 
 
 def extend_bytes(c):
-    """Algorithmic bytes of the closest-hit walk kernel: per node visit one 32 B
-    TravRec, per triangle test 60 B (3 x u32 + 3 x 16 B in reference layout),
-    per BLAS entry 88 B, plus per ray 48 B of ray state in and 32 B of hit out."""
+    """Algorithmic bytes of the closest-hit walk kernel: per node visit 32 B
+    (node + link), per triangle test 60 B (3 x u32 + 3 x 16 B in reference
+    layout), per BLAS entry 88 B, plus per ray 48 B of ray state in and 32 B
+    of hit out."""
     visits, tris, enters, queries = int(c[1]), int(c[2]), int(c[3]), int(c[4])
     return 32 * visits + 60 * tris + 88 * enters + 80 * queries
 
 
-def cpu_baseline(assets, frame):
-    """Reference baseline_render (main.cc:12) on this host, bounded sample."""
+def hierarchy_roofline(ent, launch_s, bytes_per_launch):
+    """Time floor of one walk launch from its PMC counts and the ceilings
+    measured on this GPU for the walk's own access shape (random 16-B-per-lane
+    gathers, tools/ta_probe.hip -> profiles/r02_probe/ceilings.json):
+
+      vmem_issue  wave-level vector-memory instructions (SQ_INSTS_VMEM) vs the
+                  per-CU issue floor (one per ~7.5 ns whatever the active lanes)
+      l2          L2 line requests (TCC_HIT + TCC_MISS) vs the L2-resident
+                  random-line rate
+      fabric      L2 misses (TCC_MISS) vs the Infinity-Cache-resident
+                  random-line rate
+      hbm         HBM-side bytes (FETCH_SIZE x 2 + WRITE_SIZE, the guide's
+                  gfx950 correction) vs 8 TB/s
+
+    Each level's time is count / rate; the largest is the floor t_min and
+    names the bound.  frac = t_min / measured time (<= 1 by construction when
+    the ceilings hold).  The algorithmic bytes over t_min give the effective
+    peak those bytes could be served at."""
+    try:
+        with open(CEILINGS) as fh:
+            ceil = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    pmc = ent["per_dispatch_avg"]
+    d = ent["derived"]
+    levels = {}
+
+    def level(name, count, rate, unit):
+        t = count / rate
+        levels[name] = {"count": count, "unit": unit, "ceiling_per_s": rate, "seconds": t, "frac": t / launch_s}
+
+    level("vmem_issue", pmc["SQ_INSTS_VMEM"], ceil["vmem_issue_per_s"], "wave-instructions")
+    level("l2", pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"], ceil["l2_lines_per_s"], "64-B line requests")
+    level("fabric", pmc["TCC_MISS_sum"], ceil["ic_lines_per_s"], "64-B line requests (L2 misses)")
+    level("hbm", d["hbm_side_bytes"], HBM_PEAK_GBS * 1e9, "bytes")
+    bound = max(levels, key=lambda k: levels[k]["seconds"])
+    t_min = levels[bound]["seconds"]
+    return {"bound": bound, "t_min_s": t_min, "peak_GBps": bytes_per_launch / t_min / 1e9, "levels": levels,
+            "ceilings_source": os.path.relpath(CEILINGS, ROOT)}
+
+
+def host_topology():
+    """lscpu sockets/cores/model, nproc, this job's cgroup CPU quota and affinity."""
+    import subprocess
+    topo = {}
+    try:
+        out = subprocess.run(["lscpu"], stdout=subprocess.PIPE, text=True, timeout=30).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k = k.strip()
+            if k in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)", "NUMA node(s)"):
+                topo[k] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        topo["nproc"] = int(subprocess.run(["nproc"], stdout=subprocess.PIPE, text=True, timeout=30).stdout)
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        topo["cgroup_cpu_quota"] = None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        topo["cgroup_cpu_quota"] = None
+    aff = sorted(os.sched_getaffinity(0))
+    topo["affinity_cpus"] = len(aff)
+    topo["_first_cpu"] = aff[0] if aff else 0
+    return topo
+
+
+def cpu_baseline(assets, frame, heavy_frame):
+    """Reference baseline_render (main.cc:12) on this host, bounded samples:
+    one socket's worth of OpenMP threads on frame `frame` and `heavy_frame`
+    (1280x720 x 16 spp: Msamples/s is nearly SPP-invariant), and BASELINE
+    configs[0] (frame 0, 640x360 x 32 spp) on one pinned core."""
     from oracle import Reference
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    topo = host_topology()
+    try:
+        socket_cores = int(topo["Core(s) per socket"])
+    except (KeyError, ValueError):
+        socket_cores = os.cpu_count() or 1
+    quota = topo.get("cgroup_cpu_quota")
+    threads = int(os.environ.get("PTG_CPU_THREADS", "0")) or socket_cores
     ref = Reference("v3", 1280, 720, 16, 4)
     if not ref.available():
         return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference",
                 "sample": "unavailable: %s not built" % ref.exe}
-    r = ref.baseline(assets, frame, threads=threads, timeout=900)
-    return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": r["threads"], "kind": "reference",
-            "sample": "frame %d, 1280x720 x 16 spp (%.1f M samples, full frame) through the reference's own "
-                      "baseline_render (main.cc:12-46, OpenMP static schedule) built from /root/reference sources "
-                      "with the reference flags (-O3 -ffast-math, -march=x86-64-v3); render %.2f s"
-                      % (frame, 1280 * 720 * 16 / 1e6, r["render_s"])}
+    r0 = ref.baseline(assets, frame, threads=threads, timeout=900)
+    rh = ref.baseline(assets, heavy_frame, threads=threads, timeout=900) if heavy_frame is not None else None
+    cores = min(threads, int(quota)) if quota else threads    # CPU time the job may use per second
+    out = {"value": round(r0["msamples_per_s"], 4), "unit": "Msamples/s", "cores": cores, "kind": "reference",
+           "sample": "frame %d, 1280x720 x 16 spp (14.7 M samples, full frame) through the reference's own "
+                     "baseline_render (main.cc:12-46, OpenMP static schedule) built from /root/reference sources "
+                     "with the reference flags (-O3 -ffast-math, -march=x86-64-v3); %d OpenMP threads = one socket's "
+                     "cores, on a job limited to %s CPUs of time; render %.2f s"
+                     % (frame, threads, quota if quota else "all", r0["render_s"]),
+           "threads": threads,
+           "host": {k: v for k, v in topo.items() if not k.startswith("_")}}
+    if quota and quota < socket_cores:
+        est = r0["msamples_per_s"] / quota * socket_cores
+        out["socket_estimate"] = {
+            "value": round(est, 3), "cores": socket_cores,
+            "basis": "the measured rate per CPU of quota x the %d cores of one socket (linear; this job may not "
+                     "use more than %s CPUs of time, so a whole socket cannot be timed here)" % (socket_cores, quota)}
+    if rh:
+        out["heavy_frame"] = {"frame": heavy_frame, "value": round(rh["msamples_per_s"], 4), "threads": threads,
+                              "render_s": round(rh["render_s"], 3)}
+    ref0 = Reference("v3", 640, 360, 32, 4)
+    if ref0.available():
+        c0 = ref0.baseline(assets, 0, threads=1, timeout=600, cpus=[topo["_first_cpu"]], bind="true")
+        out["config0_one_core"] = {"value": round(c0["msamples_per_s"], 4), "unit": "Msamples/s", "cores": 1,
+                                   "sample": "BASELINE configs[0]: frame 0, 640x360 x 32 spp (7.37 M samples), "
+                                             "OMP_NUM_THREADS=1 pinned to CPU %d; render %.2f s"
+                                             % (topo["_first_cpu"], c0["render_s"])}
+    return out
+
+
+def spot_rects(frame, w, h):
+    """Three 2x2 rectangles per animation frame (centre + two frame-dependent)."""
+    a = (frame * 2654435761) & 0xFFFFFFFF
+    b = (a * 2246822519 + 374761393) & 0xFFFFFFFF
+    return [(w // 2 - 1, h // 2 - 1, 2, 2), (a % (w - 2), (a >> 16) % (h - 2), 2, 2),
+            (b % (w - 2), (b >> 16) % (h - 2), 2, 2)]
 
 
 def main():
@@ -117,6 +235,8 @@ def main():
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames")
     ap.add_argument("--tile", type=str, default="32x16")
+    ap.add_argument("--concurrency", type=int, default=2, choices=[0, 1, 2],
+                    help="ptg_set_concurrency level of the timed steps (profiling passes use 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
@@ -126,9 +246,14 @@ def main():
                          "(dragon + buddha in view) in pixel tiles")
     ap.add_argument("--no-frame-setup", action="store_true",
                     help="skip the second (PCIe-inclusive, per-frame host setup) timing loop")
-    ap.add_argument("--animation", type=int, default=0, metavar="K",
-                    help="also render K frames spread evenly over the whole animation (frame-parallel over the "
-                         "ranks) and report frames/min for the full animation (BASELINE config 4)")
+    ap.add_argument("--heavy-frame", type=int, default=450,
+                    help="also time this frame at the same configuration (-1: skip)")
+    ap.add_argument("--animation", type=int, default=None, metavar="K",
+                    help="render K frames spread evenly over the whole animation (frame-parallel over the ranks), "
+                         "write them as BMPs and report frames/min (default 16 at the metric config, else 0)")
+    ap.add_argument("--frames-dir", default=None, help="where the animation BMPs go (default: a temp directory)")
+    ap.add_argument("--spots-out", default=None,
+                    help="npz of every animation frame's spot rectangles (default gpurun_out/anim_spots_r<rank>.npz)")
     args = ap.parse_args()
     if args.config == 1:
         args.width, args.height, args.spp, args.frame = 1280, 720, 256, 0
@@ -139,6 +264,10 @@ def main():
         args.animation = args.animation or 30
     elif args.config == 4:
         args.width, args.height, args.spp, args.frame, args.shard = 3840, 2160, 4096, 690, "tiles"
+        args.heavy_frame = -1
+    is_metric = (args.width, args.height, args.spp) == (1280, 720, 1024)
+    if args.animation is None:
+        args.animation = 16 if is_metric else 0
 
     import numpy as np
     import torch
@@ -172,6 +301,7 @@ def main():
     r = GpuRenderer(local)
     stream = torch.cuda.current_stream(local)
     r.set_stream(stream)
+    r.set_concurrency(args.concurrency)
     tw, th = [int(v) for v in args.tile.split("x")]
     frame = args.frame + (rank if args.shard == "frames" else 0)
 
@@ -195,9 +325,17 @@ def main():
 
     long_steps = cfg.width * cfg.height * cfg.samples_per_pixel > 4e9
 
-    def timed(fn, timing):
+    def reduce_max(v):
+        if world > 1:
+            t = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            v = float(t.item())
+        return v
+
+    def timed(fn, timing, steps=None, warmup=None):
         """K steps of fn between barrier + synchronize on both sides; max over ranks."""
-        for _ in range(args.warmup):
+        steps = args.steps if steps is None else steps
+        for _ in range(args.warmup if warmup is None else warmup):
             fn()
         torch.cuda.synchronize(local)
         if world > 1:
@@ -205,39 +343,68 @@ def main():
         torch.cuda.synchronize(local)
         r.enable_timing(timing)
         t0 = time.perf_counter()
-        for k in range(args.steps):
+        for k in range(steps):
             fn()    # asynchronous: host work of step k+1 overlaps the kernels of step k
             if long_steps:   # progress for multi-minute configurations (completes step k-1 first)
-                print("step %d/%d issued at %.1f s" % (k + 1, args.steps, time.perf_counter() - t0),
+                print("step %d/%d issued at %.1f s" % (k + 1, steps, time.perf_counter() - t0),
                       file=sys.stderr, flush=True)
         torch.cuda.synchronize(local)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(local)
         el = time.perf_counter() - t0
-        kt = r.kernel_times() if timing else {}
+        kb = r.kernel_busy() if timing else {}
         r.enable_timing(False)
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearse else dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el, kt
+        return reduce_max(el), kb
 
     # (1) the metric: render steps over a frame whose inputs are resident in HBM
-    elapsed, kt = timed(render_step, True)
-    # per-kernel device times of the K timed steps (HIP events recorded on the launch stream)
-    step_kernel_ms = {k: v[0] for k, v in kt.items() if v[1]}
-    step_kernel_n = {k: v[1] for k, v in kt.items() if v[1]}
+    elapsed, kb = timed(render_step, True)
+    # per-kernel device time of the K timed steps (HIP events on the launch streams):
+    # busy = union of a kind's launch intervals (overlapping launches counted once)
+    step_busy_ms = {k: v[0] for k, v in kb.items() if v[2]}
+    step_sum_ms = {k: v[1] for k, v in kb.items() if v[2]}
+    step_launches = {k: v[2] for k, v in kb.items() if v[2]}
     # (2) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
     elapsed_frame = None if args.no_frame_setup else timed(frame_step, False)[0]
 
+    samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
+    value = samples_per_step * args.steps / elapsed / 1e6
+    value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
+
+    # (3) the heavy companion frame at the same configuration
+    heavy = None
+    if args.heavy_frame >= 0:
+        hf = args.heavy_frame + (rank if args.shard == "frames" else 0)
+        scene.setup_frame(hf)
+        r.upload(scene, include_static=False)
+        hsteps = max(1, min(args.steps, 3))
+        el_h, _ = timed(render_step, False, steps=hsteps, warmup=1)
+        heavy = {"frame": args.heavy_frame, "value": round(samples_per_step * hsteps / el_h / 1e6, 3),
+                 "unit": "Msamples/s", "ms_per_step": round(el_h / hsteps * 1e3, 3), "steps": hsteps}
+
+    # (4) the animation (BASELINE config 4): K frames spread evenly over all 1800 (frame
+    # cost varies ~7x), frame-parallel over the ranks; each frame is set up on the host,
+    # uploaded, rendered, copied back and written as a BMP by a writer thread while the
+    # next frame renders (main.cc:78-101)
     anim = None
     if args.animation > 0:
-        # BASELINE config 4: the animation frame-parallel over the ranks, one frame
-        # per GPU at a time; K frames spread evenly over all 1800 (frame cost varies ~7x)
+        import tempfile
+        from concurrent.futures import ThreadPoolExecutor
         total_frames = scene.frame_count()
         picks = [round(i * total_frames / args.animation) % total_frames for i in range(args.animation)]
         mine = picks[rank::world]
+        frames_dir = args.frames_dir or tempfile.mkdtemp(prefix="ptg_frames_")
+        os.makedirs(frames_dir, exist_ok=True)
+        acc_img = torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device=dev)
+        host = [torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        pending = [None, None]
+        spots = {"frames": [], "rects": [], "acc_bits": [], "bgra": []}
+        writer = ThreadPoolExecutor(1)
+
+        def write(path, buf, ev):
+            ev.synchronize()
+            N.write_bmp(path, buf.numpy())
+
         torch.cuda.synchronize(local)
         if world > 1:
             dist.barrier()
@@ -247,36 +414,58 @@ def main():
         for k, f in enumerate(mine):
             scene.setup_frame(f)
             r.upload(scene, include_static=False)
-            r.render(cfg, out_bgra=image)
+            r.render(cfg, out_bgra=image, out_accum=acc_img)
             marks[k + 1].record(stream)
+            b = k % 2
+            if pending[b] is not None:
+                pending[b].result()             # the writer is done with this staging buffer
+            host[b].copy_(image, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            pending[b] = writer.submit(write, os.path.join(frames_dir, "frame_%04d.bmp" % f), host[b], ev)
+            for x0, y0, rw, rh in spot_rects(f, cfg.width, cfg.height):
+                # device-side copies (asynchronous, in stream order); read back after the loop
+                spots["frames"].append(f)
+                spots["rects"].append((x0, y0, rw, rh))
+                spots["acc_bits"].append(acc_img[y0:y0 + rh, x0:x0 + rw, :3].clone())
+                spots["bgra"].append(image[y0:y0 + rh, x0:x0 + rw].clone())
+        for p in pending:
+            if p is not None:
+                p.result()
         torch.cuda.synchronize(local)
         per_frame = sorted(((marks[k].elapsed_time(marks[k + 1]), f) for k, f in enumerate(mine)), reverse=True)
+        writer.shutdown()
         if world > 1:
             dist.barrier()
-        anim_s = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([anim_s], dtype=torch.float64, device="cpu" if rehearse else dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            anim_s = float(t.item())
+        anim_s = reduce_max(time.perf_counter() - t0)
+        spots_out = args.spots_out or os.path.join(ROOT, "gpurun_out", "anim_spots_r%d.npz" % rank)
+        os.makedirs(os.path.dirname(spots_out), exist_ok=True)
+        np.savez_compressed(spots_out, frames=np.array(spots["frames"], np.int32),
+                            rects=np.array(spots["rects"], np.int32),
+                            acc_bits=np.array([t.cpu().numpy().view(np.uint32) for t in spots["acc_bits"]]),
+                            bgra=np.array([t.cpu().numpy() for t in spots["bgra"]]), width=cfg.width, height=cfg.height,
+                            spp=cfg.samples_per_pixel, bounces=cfg.max_bounces)
+        bmps = sum(1 for f in mine if os.path.exists(os.path.join(frames_dir, "frame_%04d.bmp" % f)))
         anim = {"frames_per_min": round(len(picks) / anim_s * 60.0, 3),
                 "full_animation_min": round(total_frames / (len(picks) / anim_s * 60.0), 2),
                 "msamples_per_s": round(len(picks) * cfg.width * cfg.height * cfg.samples_per_pixel / anim_s / 1e6, 3),
                 "frames": len(picks), "frame_stride": total_frames // max(1, args.animation),
-                "seconds": round(anim_s, 3),
+                "seconds": round(anim_s, 3), "bmps_written": bmps, "frames_dir": frames_dir,
+                "spots": os.path.relpath(spots_out, ROOT) if spots_out.startswith(ROOT) else spots_out,
                 "slowest_frames_ms": [[f, round(ms, 1)] for ms, f in per_frame[:5]],
-                "step": "setup_animation_frame + per-frame upload + render per frame, frames dealt to ranks round-robin"}
+                "step": "setup_animation_frame + per-frame upload + render + BMP write (writer thread, overlapped "
+                        "with the next frame) per frame; frames dealt to ranks round-robin; spot rectangles of "
+                        "every frame checked against the oracle by tests/test_animation_spots.py"}
 
-    samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
-    value = samples_per_step * args.steps / elapsed / 1e6
-    value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
-
-    is_metric = (cfg.width, cfg.height, cfg.samples_per_pixel) == (1280, 720, 1024)
     workload = "frame %d, %dx%d, %d spp, %d bounces" % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel,
                                                          cfg.max_bounces)
     result = None
     if rank == 0:
         roof = None
         if not args.no_roofline:
+            if heavy is not None or anim is not None:   # back to the metric frame for the counting passes
+                scene.setup_frame(frame)
+                r.upload(scene, include_static=False)
             # deterministic work counters of the same render (separate counting pass, untimed)
             if long_steps:
                 print("counting pass", file=sys.stderr, flush=True)
@@ -291,16 +480,10 @@ def main():
             total = sum(kc[k] for k in kc)
             per_step_samples = int(total[0])
             # dominant kernel: the closest-hit BVH walk (k_wf_walk<closest>, "extend")
-            ext_ms, ext_n = step_kernel_ms["extend"], step_kernel_n["extend"]
-            ext_bytes = extend_bytes(kc["extend"])
-            ms_per_launch = ext_ms / ext_n
-            bytes_per_launch = ext_bytes / (ext_n / args.steps)
-            achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9
-            # whole hot path per step: wall time of the timed steps (the sky kernel runs
-            # on a second stream, overlapped with the walks, so kernel times do not add up)
-            path_ms = elapsed / args.steps * 1e3
-            path_bytes = algorithmic_bytes(total)
-            traffic, traffic_src = pmc_traffic("extend", workload, ms_per_launch)
+            ext_bytes = extend_bytes(kc["extend"])                  # algorithmic bytes per step
+            launches = step_launches["extend"] / args.steps
+            busy_ms = step_busy_ms["extend"] / args.steps            # union of its launch intervals per step
+            achieved = ext_bytes / (busy_ms * 1e-3) / 1e9
             # the same kernel with nothing beside it: one untimed render with every
             # kernel on one stream (the timed steps run up to 4 kernels at once)
             if long_steps:
@@ -312,25 +495,46 @@ def main():
             else:
                 r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
             r.synchronize()
-            kt_iso = r.kernel_times()
+            kb_iso = r.kernel_busy()
             r.enable_timing(False)
-            r.set_concurrency(2)
-            iso_ms = kt_iso["extend"][0] / max(1, kt_iso["extend"][1])
-            iso_bytes = ext_bytes / max(1, kt_iso["extend"][1])   # one render's bytes over its launches
+            r.set_concurrency(args.concurrency)
+            iso_ms = kb_iso["extend"][1] / max(1, kb_iso["extend"][2])
+            iso_bytes = ext_bytes / max(1, kb_iso["extend"][2])     # one launch's algorithmic bytes
             iso_achieved = iso_bytes / (iso_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "traffic_source": traffic_src and ("%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
-                                                       "this workload, per launch)" % traffic_src),
+            ent, prof_src = pmc_profile("extend", workload, iso_ms)
+            hier = hierarchy_roofline(ent, iso_ms * 1e-3, iso_bytes) if ent else None
+            path_ms = elapsed / args.steps * 1e3
+            path_bytes = algorithmic_bytes(total)
+            roof = {"bound": hier["bound"] if hier else "hbm",
+                    "achieved": round(achieved, 2),
+                    "peak": round(hier["peak_GBps"], 2) if hier else HBM_PEAK_GBS,
+                    "unit": "GB/s",
+                    "frac": round(hier["t_min_s"] * launches / (busy_ms * 1e-3), 5) if hier else
+                    round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": int(ent["derived"]["hbm_side_bytes"]) if ent else None,
+                    "traffic_source": prof_src and ("%s (rocprofv3 --pmc passes of this workload, per launch: "
+                                                    "FETCH_SIZE x 1 KiB x 2 + WRITE_SIZE x 1 KiB)" % prof_src),
                     "kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)",
-                    "ms_per_launch": round(ms_per_launch, 4), "launches_per_step": ext_n / args.steps,
-                    "bytes_per_launch": int(bytes_per_launch),
-                    "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_kernel_ms.items()},
+                    "basis": "achieved = the walk's algorithmic bytes per step (SURVEY 8(d) terms from the "
+                             "counting pass) / its busy time per step (union of its launch intervals, HIP events "
+                             "on the launch streams; the two chunk pipelines' walks overlap and are counted "
+                             "once); peak = those bytes / the launch's time floor over the memory-hierarchy "
+                             "levels (see 'levels': counts from the PMC profile, ceilings measured for the "
+                             "walk's access shape); frac = floor / measured time",
+                    "ms_per_launch": round(busy_ms / launches, 4), "launches_per_step": launches,
+                    "bytes_per_launch": int(ext_bytes / launches),
+                    "kernel_busy_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_busy_ms.items()},
+                    "kernel_sum_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_sum_ms.items()},
                     "isolated": {"ms_per_launch": round(iso_ms, 4), "achieved": round(iso_achieved, 2),
-                                 "frac": round(iso_achieved / HBM_PEAK_GBS, 5),
+                                 "frac": round(hier["t_min_s"] / (iso_ms * 1e-3), 5) if hier else None,
                                  "basis": "one extra untimed render with every kernel on one stream "
-                                          "(ptg_set_concurrency(0)); the timed steps overlap the walk with the sky, "
-                                          "shadow and the other chunk's kernels, which lengthens its launches"},
+                                          "(ptg_set_concurrency(0))"},
+                    "levels": {k: {"frac_isolated": round(v["frac"], 4), "count_per_launch": v["count"],
+                                   "unit": v["unit"], "ceiling_per_s": v["ceiling_per_s"]}
+                               for k, v in hier["levels"].items()} if hier else None,
+                    "ceilings_source": hier["ceilings_source"] if hier else None,
+                    "hbm_peak_GBps": HBM_PEAK_GBS,
+                    "algorithmic_frac_of_hbm_peak": round(achieved / HBM_PEAK_GBS, 5),
                     "hot_path": {"achieved_GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
                                  "basis": "wall time per step",
                                  "algorithmic_bytes_per_sample": round(path_bytes / per_step_samples, 1),
@@ -343,7 +547,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(assets, args.frame)
+                cpu = cpu_baseline(assets, args.frame, args.heavy_frame if args.heavy_frame >= 0 else None)
             except Exception as e:  # reported, never fatal to the GPU measurement
                 cpu = {"value": None, "unit": "Msamples/s", "cores": None, "kind": "reference",
                        "sample": "failed: %s" % str(e)[:300]}
@@ -363,6 +567,7 @@ def main():
             "config": {"workload": workload + (" (BASELINE metric config)" if is_metric else ""),
                        "baseline_config": args.config,
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
+            "heavy_frame": heavy,
             "animation": anim,
             "with_frame_setup": None if value_frame is None else {
                 "value": round(value_frame, 3), "unit": "Msamples/s",
@@ -374,6 +579,10 @@ def main():
         }
         if cpu and cpu.get("value"):
             result["gpu_vs_cpu"] = round(value / cpu["value"], 2)
+            if cpu.get("socket_estimate"):
+                result["gpu_vs_cpu_socket_estimate"] = round(value / cpu["socket_estimate"]["value"], 2)
+            if heavy and cpu.get("heavy_frame"):
+                result["heavy_gpu_vs_cpu"] = round(heavy["value"] / cpu["heavy_frame"]["value"], 2)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -146,13 +146,15 @@ class Reference:
     def available(self):
         return os.path.exists(self.exe)
 
-    def run(self, assets, *args, env=None, timeout=3600):
+    def run(self, assets, *args, env=None, timeout=3600, cpus=None):
+        """Run the harness; `cpus` pins it to those host CPUs (taskset)."""
         if not self.available():
             raise FileNotFoundError(self.exe)
         e = dict(os.environ)
         if env:
             e.update(env)
-        r = subprocess.run([self.exe, assets] + [str(a) for a in args], stdout=subprocess.PIPE,
+        pin = ["taskset", "-c", ",".join(str(c) for c in cpus)] if cpus else []
+        r = subprocess.run(pin + [self.exe, assets] + [str(a) for a in args], stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, text=True, env=e, timeout=timeout)
         if r.returncode != 0:
             raise RuntimeError("ref_pt %s failed (%d): %s" % (args, r.returncode, r.stderr[-2000:]))
@@ -182,10 +184,15 @@ class Reference:
     def dump(self, assets, frame, outdir):
         self.run(assets, "dump", frame, outdir)
 
-    def baseline(self, assets, frame, threads=None, timeout=3600):
-        """Times the reference's own baseline_render (main.cc:12) on this host."""
+    def baseline(self, assets, frame, threads=None, timeout=3600, cpus=None, bind=None):
+        """Times the reference's own baseline_render (main.cc:12) on this host.
+        threads -> OMP_NUM_THREADS; cpus -> taskset pinning; bind -> OMP_PROC_BIND
+        (with OMP_PLACES=cores)."""
         import json
         with tempfile.TemporaryDirectory() as d:
-            env = {"OMP_NUM_THREADS": str(threads)} if threads else None
-            out = self.run(assets, "baseline", frame, os.path.join(d, "img.bgra"), env=env, timeout=timeout)
+            env = {"OMP_NUM_THREADS": str(threads)} if threads else {}
+            if bind:
+                env.update(OMP_PROC_BIND=bind, OMP_PLACES="cores")
+            out = self.run(assets, "baseline", frame, os.path.join(d, "img.bgra"), env=env or None, timeout=timeout,
+                           cpus=cpus)
             return json.loads(out.strip().splitlines()[-1])

@@ -25,6 +25,7 @@ REF_CONFIGS = [
     ("strict", 160, 90, 32, 4),      # small whole-frame golden
     ("strict", 1280, 720, 256, 4),   # bench workload: per-sample spot checks
     ("v3", 1280, 720, 16, 4),        # CPU baseline (reference flags, portable -march)
+    ("v3", 640, 360, 32, 4),         # CPU baseline configs[0] (one core); strict-vs-shipped statistics
 ]
 # reference host code + ptg_render in place of baseline_render (oracle/dropin_main.cc)
 DROPIN_CONFIGS = [("strict", 160, 90, 32, 4)]

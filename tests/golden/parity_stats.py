@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Parity statistics of the reference AS SHIPPED against the strict build
+(SURVEY 8(c) tiers T1-T3, verdict r1 item 7).
+
+The GPU path reproduces the reference's strict-IEEE build bit for bit
+(tests/test_gpu_*.py).  The reference's own Makefile builds with -O3
+-ffast-math -march=native (Makefile:2), which changes its arithmetic - and
+its scene arrays (normals, albedo, the BVH) - so the fair question is how far
+the shipped build is from the strict one: these are then exactly the
+GPU-vs-shipped numbers.  Both builds are the reference's own sources
+(oracle/Makefile, REF_MODE=strict and v3 = the shipped flags with a portable
+-march), run at 640x360 x 32 spp.
+
+  T1  fraction of (pixel, sample) radiances within 1e-4 relative (all three
+      channels; |a - b| <= 1e-4 max(|a|, |b|))
+  T2  fraction of pixels whose averaged radiance (j-ordered float32 sum / SPP,
+      main.cc:24-42) is within 1e-4 relative; relative difference of the image
+      means per channel
+  T3  PSNR of the tonemapped 8-bit images at full resolution (validator.py's
+      formula, validator.py:43-54, without its 2x downscale: both images are
+      at the same resolution) and the fraction of byte-identical pixels
+
+Usage: python tests/golden/parity_stats.py [--frames 0 450] [--rows y0 y1]
+writes tests/golden/parity_stats.json (whole frames by default).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+W, H, SPP, BOUNCES = 640, 360, 32, 4
+REL = 1e-4
+
+
+def within(a, b, rel=REL):
+    return np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b))
+
+
+def accumulate(samples, spp):
+    """baseline_render's per-pixel sum in sample order, float32, then / SPP."""
+    acc = np.zeros(samples.shape[:2] + (3,), np.float32)
+    for j in range(samples.shape[2]):
+        acc = acc + samples[:, :, j, :3]
+    return acc / np.float32(spp)
+
+
+def tonemap(acc):
+    from oracle import tonemap as orc_tonemap
+    flat = np.concatenate([acc.reshape(-1, 3), np.zeros((acc.shape[0] * acc.shape[1], 1), np.float32)], 1)
+    return orc_tonemap(flat).reshape(acc.shape[0], acc.shape[1], 4)
+
+
+def psnr(a, b):
+    mse = np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)
+    return float("inf") if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse))
+
+
+def frame_stats(assets, frame, y0, y1):
+    from oracle import Reference
+    samples = {}
+    for mode in ("strict", "v3"):
+        ref = Reference(mode, W, H, SPP, BOUNCES)
+        if not ref.available():
+            raise FileNotFoundError(ref.exe)
+        samples[mode] = ref.samples(assets, frame, 0, y0, W, y1 - y0, 0, SPP)[..., :3]
+    s, v = samples["strict"], samples["v3"]
+    t1 = within(s, v).all(-1)
+    acc_s, acc_v = accumulate(s, SPP), accumulate(v, SPP)
+    t2 = within(acc_s, acc_v).all(-1)
+    mean_s = acc_s.reshape(-1, 3).mean(0, dtype=np.float64)
+    mean_v = acc_v.reshape(-1, 3).mean(0, dtype=np.float64)
+    img_s, img_v = tonemap(acc_s), tonemap(acc_v)
+    return {
+        "frame": frame, "rows": [y0, y1], "samples": int(t1.size), "pixels": int(t2.size),
+        "T1_samples_within_1e-4": round(float(t1.mean()), 5),
+        "T2_pixels_within_1e-4": round(float(t2.mean()), 5),
+        "T2_image_mean_rel_diff": [round(float(x), 7) for x in np.abs(mean_v - mean_s) / np.abs(mean_s)],
+        "T3_psnr_db": round(psnr(img_s[..., :3], img_v[..., :3]), 3),
+        "T3_pixels_byte_exact": round(float((img_s == img_v).all(-1).mean()), 5),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, nargs="*", default=[0, 450])
+    ap.add_argument("--rows", type=int, nargs=2, default=[0, H])
+    ap.add_argument("--out", default=os.path.join(HERE, "parity_stats.json"))
+    a = ap.parse_args()
+    assets = os.path.join(ROOT, "assets")
+    res = {"config": {"width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
+                      "builds": {"strict": "-O2 -ffp-contract=off -fno-fast-math (== the GPU path, bit for bit)",
+                                 "v3": "-O3 -ffast-math -march=x86-64-v3 (the reference Makefile's flags, "
+                                       "portable -march)"}},
+           "frames": [frame_stats(assets, f, *a.rows) for f in a.frames]}
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
