@@ -33,7 +33,7 @@
  * Compile the including file with hipcc for gfx950 and with the flags that
  * make the arithmetic the reference's IEEE arithmetic:
  *   hipcc --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
- *         -fhip-fp32-correctly-rounded-divide-sqrt \
+ *         -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize \
  *         -I<repo>/include -I<repo>/<package>/csrc
  */
 #ifndef PTG_DEVICE_H

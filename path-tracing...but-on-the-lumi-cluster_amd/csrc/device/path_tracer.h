@@ -56,6 +56,7 @@ constexpr int SECONDARY_ITERATIONS = 4;
 
 struct Counters {
     uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0, iters = 0;
+    uint32_t step_loads = 0;   // PTG_VMEM_STATS: loads of the last step (1 record, 2 triangle, 4 instance)
 };
 
 struct Hit {
@@ -272,6 +273,68 @@ struct WalkerT {
         return nearv <= farv && farv > tmin && nearv < tmax;
     }
 
+    // ray_query_enter_blas (ray_query.hh:153-182) with instance `leaf`'s record:
+    // rows M0..M3 of inv_transform in xyz; w: blas count, offset, tri_base
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    PTG_D void enter(uint32_t leaf, v4f a, v4f b, v4f c, v4f e)
+    {
+        const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(b.x, b.y, b.z), M2 = V3(c.x, c.y, c.z), M3 = V3(e.x, e.y, e.z);
+        const f3 o = cold.world_o(), d = cold.world_d();
+        org = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
+                 M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
+                 M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
+        const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
+                         M0.y * d.x + M1.y * d.y + M2.y * d.z,
+                         M0.z * d.x + M1.z * d.y + M2.z * d.z);
+        const uint32_t bcount = __float_as_uint(a.w), boffset = __float_as_uint(b.w);
+        tri_base = __float_as_uint(c.w);
+        inst = leaf;
+        cold.set_resume(node);
+#if PTG_FAST_RCP
+        bool ok = true;   // one fallback branch for the four reciprocals of the entry
+        inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
+#else
+        inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+#endif
+        base = boffset * 8 + octant(bd) * bcount;
+        count = bcount;
+        node = 0;
+        // ray_triangle_intersection_preprocess (math.hh:340-356)
+        const float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
+        f3 rd = bd;
+        axis = 2;
+        if(ax > ay && ax > az) { axis = 0; rd = V3(bd.z, bd.y, bd.x); }
+        else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
+#if PTG_FAST_RCP
+        float k = rcp_nr(rd.z, ok);
+        if(!ok)
+        {   // a zero, denormal or huge component (rare): IEEE division
+            inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
+            k = 1.0f / rd.z;
+        }
+#else
+        const float k = 1.0f / rd.z;
+#endif
+        S = V3(rd.x * k, rd.y * k, 1.0f * k);
+    }
+
+    // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246,
+    // math.hh:358-401) with triangle `leaf`'s TriRec chunks
+    template<bool ANY>
+    PTG_D int tri_test(uint32_t leaf, float4 q0, float4 q1, float4 q2)
+    {
+        float u, v, t;
+        bool back;
+        if(tri_accept(org, axis, S, V3(q0.x, q0.y, q0.z), V3(q0.w, q1.x, q1.y), V3(q1.z, q1.w, q2.x), tmin, tmax, u, v, t,
+                      back))
+        {
+            if(ANY) return 2;
+            cold.confirm(u, v, t, inst, leaf, back);
+            tmax = t;
+        }
+        return 0;
+    }
+
     // One step.  Returns 0 while the walk goes on, 1 when it has ended, 2 (ANY
     // only) when an occluder was found.
     template<bool ANY, bool COUNT>
@@ -293,7 +356,7 @@ struct WalkerT {
         const float4* rq = reinterpret_cast<const float4*>(rec);
         const float4 lo2 = rq[2], hi2 = rq[3];
 #endif
-        if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; }
+        if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; cnt.step_loads |= 1u; }
         uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
         if(!box_hit(lo, hi))
         {
@@ -316,69 +379,17 @@ struct WalkerT {
         if(axis < 0)
         {
             PTG_CHECK(sc, leaf < sc.inst_count, kDebugInst);
-            // ray_query_enter_blas (ray_query.hh:153-182)
-            if(COUNT) cnt.blas_entries++;
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + leaf);
+            if(COUNT) { cnt.blas_entries++; cnt.step_loads |= 4u; }
             // whole-row vector loads: float4 members get re-split by the
             // compiler into unaligned pieces (5 loads instead of 4)
-            const v4f a = ip[0], b = ip[1], c = ip[2], e = ip[3];
-            // rows M0..M3 of inv_transform in xyz; w: blas count, offset, tri_base
-            const f3 M0 = V3(a.x, a.y, a.z), M1 = V3(b.x, b.y, b.z), M2 = V3(c.x, c.y, c.z), M3 = V3(e.x, e.y, e.z);
-            const f3 o = cold.world_o(), d = cold.world_d();
-            org = V3(M0.x * o.x + M1.x * o.y + M2.x * o.z + M3.x * 1.0f,
-                     M0.y * o.x + M1.y * o.y + M2.y * o.z + M3.y * 1.0f,
-                     M0.z * o.x + M1.z * o.y + M2.z * o.z + M3.z * 1.0f);
-            const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
-                             M0.y * d.x + M1.y * d.y + M2.y * d.z,
-                             M0.z * d.x + M1.z * d.y + M2.z * d.z);
-            const uint32_t bcount = __float_as_uint(a.w), boffset = __float_as_uint(b.w);
-            tri_base = __float_as_uint(c.w);
-            inst = leaf;
-            cold.set_resume(node);
-#if PTG_FAST_RCP
-            bool ok = true;   // one fallback branch for the four reciprocals of the entry
-            inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
-#else
-            inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
-#endif
-            base = boffset * 8 + octant(bd) * bcount;
-            count = bcount;
-            node = 0;
-            // ray_triangle_intersection_preprocess (math.hh:340-356)
-            const float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
-            f3 rd = bd;
-            axis = 2;
-            if(ax > ay && ax > az) { axis = 0; rd = V3(bd.z, bd.y, bd.x); }
-            else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
-#if PTG_FAST_RCP
-            float k = rcp_nr(rd.z, ok);
-            if(!ok)
-            {   // a zero, denormal or huge component (rare): IEEE division
-                inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
-                k = 1.0f / rd.z;
-            }
-#else
-            const float k = 1.0f / rd.z;
-#endif
-            S = V3(rd.x * k, rd.y * k, 1.0f * k);
+            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + leaf);
+            enter(leaf, ip[0], ip[1], ip[2], ip[3]);
             return 0;
         }
-        // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246, math.hh:358-401)
-        if(COUNT) cnt.tri_tests++;
+        if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
         PTG_CHECK(sc, tri_base + leaf < sc.tri_count, kDebugTri);
         const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + leaf);
-        const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-        float u, v, t;
-        bool back;
-        if(tri_accept(org, axis, S, V3(q0.x, q0.y, q0.z), V3(q0.w, q1.x, q1.y), V3(q1.z, q1.w, q2.x), tmin, tmax, u, v, t,
-                      back))
-        {
-            if(ANY) return 2;
-            cold.confirm(u, v, t, inst, leaf, back);
-            tmax = t;
-        }
-        return 0;
+        return tri_test<ANY>(leaf, tp[0], tp[1], tp[2]);
     }
 };
 

@@ -290,6 +290,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WALK_LDS
 #define PTG_WALK_LDS 1
 #endif
+#ifndef PTG_VMEM_STATS
+#define PTG_VMEM_STATS 0
+#endif
 #ifndef PTG_WF_SLOTS
 #define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
 #endif
@@ -333,6 +336,9 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
 #endif
     bool active = false;
     uint32_t q = 0;
+#if PTG_VMEM_STATS
+    uint32_t vm_rec = 0, vm_tri = 0, vm_inst = 0, vm_refill = 0;
+#endif
     for(;;)
     {
         if(cursor < end)
@@ -341,6 +347,9 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if(nidle >= (uint32_t)kRefillIdle || nidle == 64u)
             {
+#if PTG_VMEM_STATS
+                if(COUNT && lane == 0) vm_refill++;
+#endif
                 if(!active)
                 {
                     const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
@@ -378,6 +387,13 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
         if(COUNT && lane == 0) cnt.iters++;   // wave loop iterations (lane 0 counts for its wave)
 #pragma unroll
         for(int u = 0; u < PTG_WALK_UNROLL; ++u)
+        {
+#if PTG_VMEM_STATS
+        // diagnostic build: wave-level load instructions of each step by kind,
+        // counted in the walk kinds' unused slots: [0] record, [5] triangle,
+        // [6] instance, [7] refill (see tools/ablate.py --counters)
+        if(COUNT) cnt.step_loads = 0;
+#endif
         if(active)
         {
             const int r = w.template step<ANY, COUNT>(sc, cnt);
@@ -405,8 +421,22 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                 active = false;
             }
         }
+#if PTG_VMEM_STATS
+        if(COUNT)
+        {
+            const unsigned long long br = __ballot(cnt.step_loads & 1u), bt = __ballot(cnt.step_loads & 2u),
+                                     bi = __ballot(cnt.step_loads & 4u);
+            if(lane == 0) { vm_rec += br != 0; vm_tri += bt != 0; vm_inst += bi != 0; }
+        }
+#endif
+        }
     }
+#if PTG_VMEM_STATS
+    if(COUNT) { cnt.shades = vm_tri; cnt.tlas_visits = vm_inst; cnt.iters = vm_refill; }
+    if(COUNT) flush_counters(cnt, counters, vm_rec);
+#else
     if(COUNT) flush_counters(cnt, counters, 0);
+#endif
 }
 
 // Shading of one round is split by what the paths will run.

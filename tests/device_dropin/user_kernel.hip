@@ -40,17 +40,17 @@ int user_path_trace(const ptg_render_config* cfg, uint32_t n, const ptg_uint2* x
                     const ptg_bvh_link* links, const uint32_t* indices, const ptg_float3* pos,
                     const ptg_float3* normal, const ptg_float4* albedo, const ptg_float4* material, ptg_float4* out)
 {
-    if(ptg_device_set_config(cfg) != hipSuccess) return -1;
+    if(hipError_t e = ptg_device_set_config(cfg)) return -1000 - int(e);
     hipLaunchKernelGGL(k_user_samples, dim3((n + 127) / 128), dim3(128), 0, 0, n, xy, js, subframes, instances, nodes,
                        links, indices, pos, normal, albedo, material, out);
-    if(hipGetLastError() != hipSuccess) return -2;
+    if(hipError_t e = hipGetLastError()) return -2000 - int(e);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
 
 int user_tonemap_device(uint32_t n, const ptg_float4* in, ptg_uchar4* out)
 {
     hipLaunchKernelGGL(k_user_tonemap, dim3((n + 255) / 256), dim3(256), 0, 0, n, in, out);
-    if(hipGetLastError() != hipSuccess) return -2;
+    if(hipError_t e = hipGetLastError()) return -2000 - int(e);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
 
