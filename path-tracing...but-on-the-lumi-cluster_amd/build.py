@@ -65,6 +65,12 @@ def build_test_kernels(verbose=False):
     _run(["make"], os.path.join(ROOT, "tests", "device_dropin"), verbose)
 
 
+def build_tools(verbose=False):
+    """tools/_bin/walk_sim: the CPU model of the block walk over the upload's own
+    packing (tests/test_block_bvh.py)."""
+    _run(["make", "walk_sim"], os.path.join(ROOT, "tools"), verbose)
+
+
 def prepare_assets():
     from . import assets
     return assets.prepare(assets.default_dir(ROOT))
@@ -74,4 +80,5 @@ def build(verbose=False):
     prepare_assets()
     build_native(verbose)
     build_test_kernels(verbose)
+    build_tools(verbose)
     build_oracle(verbose)

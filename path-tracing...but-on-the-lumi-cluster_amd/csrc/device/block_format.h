@@ -1,0 +1,78 @@
+// Block BVH records: the walk's traversal data, shared by the host packer
+// (host/block_bvh.cpp) and the device walker (device/block_walk.h).
+//
+// The reference stores a BVH as nodes (bvh.hh:45-51, 24 B AABB) plus eight
+// stackless link orders (bvh.hh:53-67), one per ray-direction octant, and
+// walks it node by node along `accept` / `cancel`: one dependent 32 B gather
+// per node visit (ray_query.hh:184-223).  The links encode one fixed order:
+// the children of an inner node in build (BFS) order, reversed exactly when
+// the ray's direction is not positive on the node's split axis
+// (bvh.cc:173-191).  Every leaf the walk reaches is therefore met in one
+// depth-first order per octant, and a leaf is reached iff its own box test
+// and those of all its ancestors pass, each at its own time (tmax shrinks as
+// hits are confirmed).
+//
+// Two facts let a walk test far fewer boxes with the same outcome:
+//  1. Containment.  Every box contains its children's boxes (each is the
+//     fmin/fmax union of the leaf boxes below it, bvh.cc:65-80, 198-201; the
+//     packer checks it), and the slab test
+//     `near <= far && far > tmin && near < tmax` (ray_query.hh:197-207) is
+//     monotone under box inclusion in IEEE arithmetic (subtraction and
+//     multiplication by the same reciprocal are monotone; an infinite
+//     reciprocal yields a NaN only on a slab plane, where the child fails
+//     too).  So a child that passes at some tmax has a parent that passes at
+//     any tmax at least as large - in particular at the parent's own, earlier
+//     test.  Skipping inner box tests never changes which leaves are reached.
+//  2. Deferred tests.  `near` and `far` do not depend on tmax, and tmax only
+//     shrinks.  A box tested early with a larger tmax, rejected, is rejected
+//     by the reference too; accepted, it is re-checked with `near < tmax` at
+//     the time the reference would test it.
+// Leaf boxes gate the triangle tests and BLAS entries, so they are always
+// decided at their own time (fact 2); inner boxes are tested only to prune.
+//
+// Layout.  The binary SAH tree (with multi-leaf buckets) is collapsed into
+// 4-wide blocks: a block holds up to four descendants of one node (its
+// children, some replaced by their own children).  A walk step loads one
+// block (128 B, eight 16-byte loads with no dependency between them), tests
+// all four boxes, continues with the first passing entry in the ray's order
+// and pushes the others onto a per-lane stack in reverse order.  Leaf
+// entries are pushed with their `near` and re-checked when popped; inner
+// entries are pushed bare (their subtree is entered and its own boxes tested
+// then, fact 1).  Leaves are thus met in the reference's order with the
+// reference's tmax: identical hits, ties and back-face flags.
+//
+//   BlockEntry (32 B)   lo.xyz | a   hi.xyz | b
+//     a: kBeLeaf | payload   leaf (BLAS: triangle index in the mesh,
+//                            TLAS: instance index), payload < 2^28
+//        kBeNone             unused slot, never passes
+//        otherwise           block index of the child's own block
+//     b: slot order of the block: entry i holds octants 2i (bits 0-15) and
+//        2i+1 (bits 16-31); nibble j of an octant's half names the slot the
+//        ray meets j-th (unused slots last).
+// A BVH's handle is its root block's index.  One layout serves all eight
+// octants, so the records are ~13 MB for the 581k-node scene, against
+// 8 x 581k x 64 B = 298 MB of per-octant paired node records.
+#pragma once
+#include <stdint.h>
+
+namespace ptg {
+
+constexpr uint32_t kBlockWidth = 4;
+
+struct alignas(16) BlockEntry {
+    float lo_x, lo_y, lo_z;
+    uint32_t a;
+    float hi_x, hi_y, hi_z;
+    uint32_t b;
+};
+static_assert(sizeof(BlockEntry) == 32, "BlockEntry is two 16-byte loads");
+
+constexpr uint32_t kBeLeaf = 0x80000000u;
+constexpr uint32_t kBeNone = 0x40000000u;
+constexpr uint32_t kBeIndex = 0x0FFFFFFFu;   // 28-bit block indices and payloads
+// The walker's stack words are entry `a` words (a block index, or kBeLeaf |
+// payload); a leaf word sits on top of its `near` (float bits).  kBePop
+// (a leaf word no payload can produce) means "take the next stack entry".
+constexpr uint32_t kBePop = 0xFFFFFFFFu;
+
+} // namespace ptg

@@ -1,25 +1,23 @@
 // Device-side data layout in HBM (shared by the HIP kernels and the host
 // code that packs it).  See DESIGN.md "Data layout in HBM".
 //
-// The reference arrays (bvh_node 24 B + 8 link orders of 8 B, indices +
-// float3 positions) are repacked once on the GPU into records that a
-// traversal step reads with one or two 16-byte loads:
-//   TravRec   32 B  one (node, octant) pair: AABB + that octant's link.
-//                   trav[node_offset*8 + octant*node_count + i] - the same
-//                   index the reference uses for links[] (ray_query.hh:139-140),
-//                   so the link offset arithmetic carries over unchanged.
+// The reference arrays are repacked once into records a walk step reads
+// with independent 16-byte loads:
+//   BlockEntry 32 B  4-wide BVH blocks of both levels (block_format.h): one
+//                    128 B block per step, one layout for all eight octants.
 //   TriRec    48 B  the three vertex positions of triangle t of a mesh,
 //                   tris[index_offset/3 + t] (ray_query.hh:228-234 gathers
 //                   indices then positions: two dependent loads -> one).
 //   InstTrav  64 B  what ray_query_enter_blas needs (ray_query.hh:153-182):
-//                   inv_transform rows 0..3 (xyz), each with one of the BLAS
-//                   handle and the mesh's triangle base in w.
+//                   inv_transform rows 0..3 (xyz), with the BLAS root block
+//                   and the mesh's triangle base in w.
 //   InstShade 64 B  what the closest-hit shading needs (path_tracer.hh:369-392):
 //                   transform rows 0..2 xyz and the mesh offsets.
-// BLAS records live in one buffer (uploaded once); the per-frame TLAS
-// records live in a second buffer, indexed from the first frame node.
+// BLAS blocks are packed once (when an instance first names the BLAS); the
+// frame's TLAS blocks follow them in the same buffer.
 #pragma once
 #include <stdint.h>
+#include "block_format.h"
 
 namespace ptg {
 
@@ -40,26 +38,6 @@ namespace ptg {
 #ifndef PTG_NEE_LAZY
 #define PTG_NEE_LAZY 2      // shade/sky read (1) and write (2) a path's NEE records only when it has a pending NEE ray
 #endif
-#ifndef PTG_PAIR_NODES
-#define PTG_PAIR_NODES 1
-#endif
-struct alignas(16) TravRec {
-    float min_x, min_y, min_z;
-    uint32_t accept;           // top bit: leaf; payload in the low 31 bits
-    float max_x, max_y, max_z;
-    uint32_t cancel;           // next node when the box is missed / after a leaf
-#if PTG_PAIR_NODES
-    // The same fields of node `cancel` in the same link order (cancel2 =
-    // 0xFFFFFFFF when `cancel` ends the walk): a step whose box is missed
-    // tests the next node right away instead of a dependent load later.
-    float min2_x, min2_y, min2_z;
-    uint32_t accept2;
-    float max2_x, max2_y, max2_z;
-    uint32_t cancel2;
-#endif
-};
-static_assert(sizeof(TravRec) == 32 * (1 + PTG_PAIR_NODES), "TravRec is two (four) 16-byte loads");
-
 struct alignas(16) TriRec {
     float p0x, p0y, p0z, p1x;
     float p1y, p1z, p2x, p2y;
@@ -68,8 +46,9 @@ struct alignas(16) TriRec {
 static_assert(sizeof(TriRec) == 48, "TriRec is three 16-byte loads");
 
 struct alignas(16) InstTrav {
-    // row k = inv_transform.r[k].{x,y,z} in xyz; w = blas count, blas offset,
-    // triangle base, 0 for rows 0..3: four whole, aligned 16-byte loads
+    // row k = inv_transform.r[k].{x,y,z} in xyz; w = the BLAS's root block,
+    // the mesh's triangle base, 0, 0 for rows 0..3: four whole, aligned
+    // 16-byte loads
     float4 row[4];
 };
 static_assert(sizeof(InstTrav) == 64, "InstTrav is four 16-byte loads");
@@ -82,7 +61,8 @@ static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
 
 // Everything a hot-path kernel reads, passed by value as a kernel argument.
 struct DevScene {
-    const TravRec* trav;           // BVH records of both levels, index = global link index
+    const BlockEntry* blocks;      // block BVH records of both levels (block_format.h), 4 entries per block
+    const uint32_t* tlas_root;     // per subframe: its TLAS's root block
     const TriRec* tris;
     const InstTrav* inst_trav;
     const InstShade* inst_shade;
@@ -95,7 +75,9 @@ struct DevScene {
     uint32_t width, height, spp, max_bounces, student_id, blur_step;
     uint32_t subframe_count;
     // bounds of the record buffers, checked only by PTG_DEBUG builds
-    uint32_t trav_count, tri_count, inst_count;
+    uint32_t block_count, tri_count, inst_count;
+    uint2* spill;                  // LdsStack spill areas, spill_stride entries per walk lane
+    uint32_t spill_stride;
     uint32_t* debug;               // PTG_DEBUG: violation counters (kDebug* slots), else null
 };
 

@@ -65,6 +65,9 @@ struct Hit {
     bool back_face;
 };
 
+#ifndef PTG_PK_SLAB
+#define PTG_PK_SLAB 0
+#endif
 #ifndef PTG_FAST_RCP
 #define PTG_FAST_RCP 1   // the walk's reciprocals via rcp_rn (== 1.0f / x for every x, ref_math.h)
 #endif
@@ -75,13 +78,6 @@ PTG_D float wrcp(float x) { return 1.0f / x; }
 #endif
 PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : wrcp(d); }   // 1/d, 0 -> (float)1e40
 PTG_D uint32_t octant(f3 d) { return (d.x > 0 ? 1u : 0u) | (d.y > 0 ? 2u : 0u) | (d.z > 0 ? 4u : 0u); }
-
-PTG_D void load_trav(const TravRec* p, float4& lo, float4& hi)
-{
-    const float4* q = reinterpret_cast<const float4*>(p);
-    lo = q[0];
-    hi = q[1];
-}
 
 // ray_triangle_intersection (math.hh:358-401) followed by the distance test of
 // ray_query_test_triangle (ray_query.hh:243-245): true when the triangle
@@ -136,20 +132,18 @@ PTG_D bool slab_hit(f3 org, f3 inv, float tmin, float tmax, float lx, float ly, 
     return nearv <= farv && farv > tmin && nearv < tmax;
 }
 
-// Where a walk keeps its cold state - the world ray, its reciprocal, the
-// TLAS resume point and the best hit so far.  They are touched only when a
-// BLAS is entered or left and when a hit is confirmed, so a walker can keep
-// them in registers (RegCold) or, where registers decide the occupancy, in a
-// per-lane LDS slot (LdsCold, the wavefront walk kernels).
+// Where a walk keeps its cold state - the world ray and the best hit so
+// far.  They are touched only when a BLAS is entered or left and
+// when a hit is confirmed, so a walker keeps them in registers (RegCold) or,
+// where registers and LDS decide the occupancy, in a per-lane LDS slot
+// (LdsCold, the wavefront walk kernels).
 struct RegCold {
-    f3 o, d, inv_w;            // world ray and its reciprocal direction
-    uint32_t tlas_base, tlas_count, tlas_resume;
+    f3 o, d;                   // world ray
     Hit best;
 
-    PTG_D void init(f3 ro, f3 rd, f3 iw, uint32_t tb, uint32_t tc)
+    PTG_D void init(f3 ro, f3 rd, f3)
     {
-        o = ro; d = rd; inv_w = iw;
-        tlas_base = tb; tlas_count = tc; tlas_resume = 0;
+        o = ro; d = rd;
         best.thit = -1.0f;
         best.bx = best.by = best.bz = 0.0f;
         best.instance_id = 0xFFFFFFFFu;
@@ -158,11 +152,6 @@ struct RegCold {
     }
     PTG_D f3 world_o() const { return o; }
     PTG_D f3 world_d() const { return d; }
-    PTG_D void leave_blas(f3& org, f3& inv, uint32_t& base, uint32_t& node, uint32_t& count) const
-    {
-        base = tlas_base; org = o; inv = inv_w; node = tlas_resume; count = tlas_count;
-    }
-    PTG_D void set_resume(uint32_t n) { tlas_resume = n; }
     // ray_query_confirm (ray_query.hh:280-290)
     PTG_D void confirm(float u, float v, float t, uint32_t instance, uint32_t prim, bool back)
     {
@@ -177,104 +166,211 @@ struct RegCold {
     PTG_D Hit result(float) const { return best; }
 };
 
-struct WalkCold {              // one lane's LDS slot: four conflict-free b128 accesses
-    float4 o;                  // world origin xyz, TLAS record base
-    float4 d;                  // world direction xyz, TLAS node count
-    float4 inv;                // 1/direction xyz, TLAS node to resume after the BLAS
-    float4 best;               // closest hit so far: u, v, instance, primitive | back_face << 31
+struct WalkCold {              // one lane's LDS slot: two b128 accesses
+    float4 o;                  // world origin xyz
+    float4 d;                  // world direction xyz
 };
+// LDS (address space 3) pointers to clang vector types: accesses through
+// them are ds_* instructions, never flat ones the compiler would have to
+// route at run time (HIP's float4/uint2 classes cannot be assigned through
+// an address-space pointer)
+typedef float lds_f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t lds_u2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) lds_f4v lds_cold_t;   // [0] = WalkCold::o, [1] = WalkCold::d
+typedef __attribute__((address_space(3))) lds_u2v lds_uint2_t;
 
+// World ray in LDS (read at BLAS entry and exit), best hit in registers.
 struct LdsCold {
-    WalkCold* c;
+    lds_cold_t* c;
+    float bu, bv;
+    uint32_t binst, bprim;     // bprim: primitive | back_face << 31
 
-    PTG_D void init(f3 ro, f3 rd, f3 iw, uint32_t tb, uint32_t tc)
+    PTG_D void init(f3 ro, f3 rd, f3)
     {
-        c->o = make_float4(ro.x, ro.y, ro.z, __uint_as_float(tb));
-        c->d = make_float4(rd.x, rd.y, rd.z, __uint_as_float(tc));
-        c->inv = make_float4(iw.x, iw.y, iw.z, __uint_as_float(0u));
-        c->best = make_float4(0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu), __uint_as_float(0u));
+        c[0] = lds_f4v{ro.x, ro.y, ro.z, 0.0f};
+        c[1] = lds_f4v{rd.x, rd.y, rd.z, 0.0f};
+        bu = bv = 0.0f;
+        binst = 0xFFFFFFFFu;
+        bprim = 0;
     }
-    PTG_D f3 world_o() const { const float4 v = c->o; return V3(v.x, v.y, v.z); }
-    PTG_D f3 world_d() const { const float4 v = c->d; return V3(v.x, v.y, v.z); }
-    PTG_D void leave_blas(f3& org, f3& inv, uint32_t& base, uint32_t& node, uint32_t& count) const
-    {
-        const float4 wo = c->o, wd = c->d, wi = c->inv;
-        base = __float_as_uint(wo.w); org = V3(wo.x, wo.y, wo.z);
-        inv = V3(wi.x, wi.y, wi.z); node = __float_as_uint(wi.w); count = __float_as_uint(wd.w);
-    }
-    PTG_D void set_resume(uint32_t n) { c->inv.w = __uint_as_float(n); }
+    PTG_D f3 world_o() const { const lds_f4v v = c[0]; return V3(v.x, v.y, v.z); }
+    PTG_D f3 world_d() const { const lds_f4v v = c[1]; return V3(v.x, v.y, v.z); }
     // ray_query_confirm (ray_query.hh:280-290); thit is the walk's tmax, bz is
     // derived in result() with the same arithmetic
     PTG_D void confirm(float u, float v, float, uint32_t instance, uint32_t prim, bool back)
     {
-        c->best = make_float4(u, v, __uint_as_float(instance), __uint_as_float(prim | (back ? 0x80000000u : 0u)));
+        bu = u;
+        bv = v;
+        binst = instance;
+        bprim = prim | (back ? 0x80000000u : 0u);
     }
     PTG_D Hit result(float tmax) const
     {
-        const float4 b = c->best;
-        const uint32_t id = __float_as_uint(b.z), pb = __float_as_uint(b.w);
-        const bool hit = id != 0xFFFFFFFFu;
+        const bool hit = binst != 0xFFFFFFFFu;
         Hit h;
-        h.bx = b.x;
-        h.by = b.y;
-        h.bz = hit ? 1.0f - b.x - b.y : 0.0f;
+        h.bx = bu;
+        h.by = bv;
+        h.bz = hit ? 1.0f - bu - bv : 0.0f;
         h.thit = hit ? tmax : -1.0f;
-        h.instance_id = id;
-        h.primitive_id = pb & 0x7FFFFFFFu;
-        h.back_face = (pb >> 31) != 0;
+        h.instance_id = binst;
+        h.primitive_id = bprim & 0x7FFFFFFFu;
+        h.back_face = (bprim >> 31) != 0;
         return h;
     }
 };
 
-// One ray query, resumable: the walk state of ray_query (ray_query.hh:66-109)
-// for both levels, advanced one BVH step at a time by step().  ANY = true is
+// Per-lane walk stacks of (word, near) entries (block_format.h: word = a
+// block index or kBeLeaf | payload; near = the entry distance, re-checked
+// against tmax when the entry is popped).
+// PrivStack: a private array (scratch memory) for the per-lane megakernel and
+// the per-ray entry points; the host checks every frame's stack bound
+// against kCap before those kernels run.
+struct PrivStack {
+    static constexpr uint32_t kCap = 96;     // entries; put() may write one past the bound
+    uint2 v[kCap];
+    uint32_t sp;
+    PTG_D void reset() { sp = 0; }
+    PTG_D uint32_t size() const { return sp; }
+    PTG_D void reserve(uint32_t) {}
+    PTG_D void put(uint32_t k, uint2 e) { v[sp + k] = e; }   // entry sp + k, not yet pushed
+    PTG_D void advance(uint32_t k) { sp += k; }
+    PTG_D uint2 pop() { return v[--sp]; }
+};
+
+// LdsStack: the wavefront walks' stack.  The newest kRing entries of a lane
+// live in LDS (a ring, one 8-byte column per lane: slot k of a wave's 64
+// lanes is one conflict-free 512 B row); older ones spill to the lane's area
+// in HBM and come back when the stack unwinds to them.  A 12-entry ring holds
+// the whole stack for all but ~0.3 entries per query of a heavy frame.
+#ifndef PTG_LDS_STACK
+#define PTG_LDS_STACK 12
+#endif
+struct LdsStack {
+    static constexpr uint32_t kRing = PTG_LDS_STACK;
+    lds_uint2_t* s;            // the lane's ring column: slot k at s[64 * k]
+    uint2* g;                  // the lane's spill area (HBM)
+    uint32_t sp, lo, top;      // entries; lowest entry still in the ring; ring slot of entry sp
+    PTG_D void reset() { sp = lo = top = 0; }
+    PTG_D uint32_t size() const { return sp; }
+    // room for n more entries in the ring: the oldest go to HBM (rare)
+    PTG_D void reserve(uint32_t n)
+    {
+        while(sp - lo + n > kRing)
+        {
+            uint32_t slot = top + kRing - (sp - lo);
+            if(slot >= kRing) slot -= kRing;
+            const lds_u2v v = s[64u * slot];
+            g[lo] = make_uint2(v.x, v.y);
+            ++lo;
+        }
+    }
+    // entry sp + k (k < the room reserve() made), not yet pushed
+    PTG_D void put(uint32_t k, uint2 e)
+    {
+        uint32_t slot = top + k;
+        if(slot >= kRing) slot -= kRing;
+        s[64u * slot] = lds_u2v{e.x, e.y};
+    }
+    PTG_D void advance(uint32_t k)
+    {
+        top += k;
+        if(top >= kRing) top -= kRing;
+        sp += k;
+    }
+    PTG_D uint2 pop()
+    {
+        --sp;
+        top = top ? top - 1u : kRing - 1u;
+        const lds_u2v v = s[64u * top];
+        uint2 e = make_uint2(v.x, v.y);
+        if(sp < lo)
+        {   // the ring was empty: the entry comes back from HBM (the ring
+            // slot read above held nothing; top is moot in an empty ring)
+            lo = sp;
+            e = g[sp];
+        }
+        return e;
+    }
+};
+
+// x_t for t in 0..3, as two selects on t's bits: by value, so that the
+// compiler emits v_cndmask and neither branches nor indexes a stack copy
+PTG_D uint32_t sel4(uint32_t t, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3)
+{
+    const uint32_t lo = (t & 1u) ? x1 : x0;
+    const uint32_t hi = (t & 1u) ? x3 : x2;
+    return (t & 2u) ? hi : lo;
+}
+
+// One ray query over the block records (block_format.h), resumable: a step
+// is one 4-wide block (node_step, which first pops the next stack entry if
+// the walk needs one), or one triangle test or BLAS entry (leaf_step), of
+// either level - so the lanes of a wave step together whatever level each
+// is in, and a persistent kernel can swap rays between steps.  ANY = true is
 // trace_shadow_ray (path_tracer.hh:415-427): the first accepted candidate
 // ends the walk.  ANY = false is the proceed/confirm loop of trace_ray
 // (path_tracer.hh:342-349): every accepted candidate is confirmed and
-// shortens tmax.  The flat step (TLAS node, BLAS node, BLAS entry, triangle
-// test or BLAS exit) keeps the lanes of a wave stepping together whatever
-// level each one is in.
-template<class Cold>
-struct WalkerT {
-    Cold cold;                 // world ray, TLAS resume point, best hit
+// shortens tmax.  Candidates are met in the reference's order with the
+// reference's tmax (block_format.h), so the result is bit-identical to the
+// reference's stackless link walk (ray_query.hh:184-278).
+template<class Cold, class Stack>
+struct BlockWalker {
+    Cold cold;                 // world ray, best hit
+    Stack st;
     float tmin, tmax;
     f3 org, inv;               // active level: ray origin / 1/dir in that level's space
-    uint32_t base, node, count;
+    f3 winv;                   // the world ray's 1/dir (the TLAS level's inv)
+    uint32_t oct;              // active level: direction octant (the links' order index, ray_query.hh:139-140)
     f3 S;                      // BLAS: shear constants of ray_triangle_intersection_preprocess
     int axis;                  // BLAS: dominant axis, -1 while in the TLAS (blas_axis)
-    uint32_t tri_base, inst;
+    uint32_t tri_base, inst, bsp;
+    uint32_t cur;              // next block, leaf word, or kBePop
 
-    PTG_D void init(const DevScene& sc, uint32_t tc, uint32_t to, f3 ro, f3 rd, float t0, float t1)
+    // ray_query_initialize (ray_query.hh:111-151); root = the TLAS's root
+    // block, kBePop for no TLAS (the walk ends at its first step)
+    PTG_D void init(uint32_t root, f3 ro, f3 rd, float t0, float t1)
     {
         const f3 iw = V3(rcp_or_big(rd.x), rcp_or_big(rd.y), rcp_or_big(rd.z));
-        base = to * 8 + octant(rd) * tc;
-        cold.init(ro, rd, iw, base, tc);
+        cold.init(ro, rd, iw);
         tmin = t0;
         tmax = t1;
         org = ro;
         inv = iw;
-        node = 0;
-        count = tc;
+        winv = iw;
+        oct = octant(rd);
         S = V3(0, 0, 0);
         axis = -1;
         tri_base = 0;
         inst = 0xFFFFFFFFu;
+        bsp = 0;
+        st.reset();
+        cur = root;
     }
     PTG_D Hit result() const { return cold.result(tmax); }
 
-    // slab test (ray_query.hh:197-207); min/max results only feed compares
-    PTG_D bool box_hit(float4 lo, float4 hi) const
+    // slab test (ray_query.hh:197-207) with its entry distance.  PTG_PK_SLAB:
+    // the subtractions and products as packed pairs (lo, hi) per axis -
+    // v_pk_add_f32 / v_pk_mul_f32 round each lane exactly as the scalar ops
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    PTG_D bool box(float4 lo, float4 hi, float& nearv) const
     {
+#if PTG_PK_SLAB
+        const v2f tx = (v2f{lo.x, hi.x} - v2f{org.x, org.x}) * v2f{inv.x, inv.x};
+        const v2f ty = (v2f{lo.y, hi.y} - v2f{org.y, org.y}) * v2f{inv.y, inv.y};
+        const v2f tz = (v2f{lo.z, hi.z} - v2f{org.z, org.z}) * v2f{inv.z, inv.z};
+        const float t0x = tx.x, t1x = tx.y, t0y = ty.x, t1y = ty.y, t0z = tz.x, t1z = tz.y;
+#else
         const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
         const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;
         const float t0z = (lo.z - org.z) * inv.z, t1z = (hi.z - org.z) * inv.z;
-        const float nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
+#endif
+        nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
         const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
         return nearv <= farv && farv > tmin && nearv < tmax;
     }
 
     // ray_query_enter_blas (ray_query.hh:153-182) with instance `leaf`'s record:
-    // rows M0..M3 of inv_transform in xyz; w: blas count, offset, tri_base
+    // rows M0..M3 of inv_transform in xyz; w: BLAS root block, triangle base
     typedef float v4f __attribute__((ext_vector_type(4)));
     PTG_D void enter(uint32_t leaf, v4f a, v4f b, v4f c, v4f e)
     {
@@ -286,19 +382,17 @@ struct WalkerT {
         const f3 bd = V3(M0.x * d.x + M1.x * d.y + M2.x * d.z,
                          M0.y * d.x + M1.y * d.y + M2.y * d.z,
                          M0.z * d.x + M1.z * d.y + M2.z * d.z);
-        const uint32_t bcount = __float_as_uint(a.w), boffset = __float_as_uint(b.w);
-        tri_base = __float_as_uint(c.w);
+        cur = __float_as_uint(a.w);
+        tri_base = __float_as_uint(b.w);
         inst = leaf;
-        cold.set_resume(node);
+        bsp = st.size();
+        oct = octant(bd);
 #if PTG_FAST_RCP
         bool ok = true;   // one fallback branch for the four reciprocals of the entry
         inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
 #else
         inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
 #endif
-        base = boffset * 8 + octant(bd) * bcount;
-        count = bcount;
-        node = 0;
         // ray_triangle_intersection_preprocess (math.hh:340-356)
         const float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
         f3 rd = bd;
@@ -335,74 +429,137 @@ struct WalkerT {
         return 0;
     }
 
-    // One step.  Returns 0 while the walk goes on, 1 when it has ended, 2 (ANY
-    // only) when an occluder was found.
-    template<bool ANY, bool COUNT>
-    PTG_D int step(const DevScene& sc, Counters& cnt)
+    PTG_D bool at_leaf() const { return (cur & kBeLeaf) && cur != kBePop; }
+
+    // Node phase: pop the next entry if the walk needs one, then, if it is a
+    // block, one block step.  Returns 1 when the walk has ended, else 0 (the
+    // walk may then stand at a leaf, which leaf_step() takes).
+    template<bool COUNT>
+    PTG_D int node_step(const DevScene& sc, Counters& cnt)
     {
-        if(node >= count)
+        if(cur == kBePop)
         {
-            if(axis < 0) return 1;
-            // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
-            axis = -1;
-            cold.leave_blas(org, inv, base, node, count);
-            return 0;
+            for(;;)
+            {
+                if(st.size() == (axis < 0 ? 0u : bsp))
+                {
+                    if(axis < 0) return 1;
+                    // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
+                    axis = -1;
+                    org = cold.world_o();
+                    inv = winv;
+                    oct = octant(cold.world_d());
+                    continue;
+                }
+                const uint2 e = st.pop();
+                if(__uint_as_float(e.y) < tmax) { cur = e.x; break; }   // the entry's test at its own time
+            }
+            if(cur & kBeLeaf) return 0;
         }
-        PTG_CHECK(sc, base + node < sc.trav_count, kDebugNode);
-        float4 lo, hi;
-        const TravRec* rec = sc.trav + (base + node);
-        load_trav(rec, lo, hi);
-#if PTG_PAIR_NODES
-        const float4* rq = reinterpret_cast<const float4*>(rec);
-        const float4 lo2 = rq[2], hi2 = rq[3];
-#endif
-        if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; cnt.step_loads |= 1u; }
-        uint32_t accept = __float_as_uint(lo.w), cancel = __float_as_uint(hi.w);
-        if(!box_hit(lo, hi))
+        const uint32_t w = cur;
+        PTG_CHECK(sc, w < sc.block_count, kDebugNode);
+        // one block: four boxes, eight independent 16-byte loads
+        const v4f* p = reinterpret_cast<const v4f*>(sc.blocks + size_t(w) * kBlockWidth);
+        const v4f q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4], q5 = p[5], q6 = p[6], q7 = p[7];
+        const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q1.x, q1.y, q1.z, q1.w);
+        const float4 l1 = make_float4(q2.x, q2.y, q2.z, q2.w), h1 = make_float4(q3.x, q3.y, q3.z, q3.w);
+        const float4 l2 = make_float4(q4.x, q4.y, q4.z, q4.w), h2 = make_float4(q5.x, q5.y, q5.z, q5.w);
+        const float4 l3 = make_float4(q6.x, q6.y, q6.z, q6.w), h3 = make_float4(q7.x, q7.y, q7.z, q7.w);
+        if(COUNT) cnt.step_loads |= 1u;
+        uint32_t b0 = __float_as_uint(h0.w), b1 = __float_as_uint(h1.w), b2 = __float_as_uint(h2.w), b3 = __float_as_uint(h3.w);
+        // keep the order words in the registers the block load filled (the
+        // compiler would otherwise re-load the one the select picks)
+        asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+        const uint32_t ob = oct >> 1;
+        const uint32_t pw = ob < 2u ? (ob ? b1 : b0) : (ob == 3u ? b3 : b2);
+        const uint32_t perm = (oct & 1u) ? pw >> 16 : pw;
+        const uint32_t a0 = __float_as_uint(l0.w), a1 = __float_as_uint(l1.w), a2 = __float_as_uint(l2.w),
+                       a3 = __float_as_uint(l3.w);
+        float n0, n1, n2, n3;
+        const bool p0 = box(l0, h0, n0) && !(a0 & kBeNone), p1 = box(l1, h1, n1) && !(a1 & kBeNone);
+        const bool p2 = box(l2, h2, n2) && !(a2 & kBeNone), p3 = box(l3, h3, n3) && !(a3 & kBeNone);
+        if(COUNT)
         {
-#if PTG_PAIR_NODES
-            // missed: the next node in link order is `cancel`, whose record came
-            // with this one - test it now, exactly as the next step would
-            if(cancel >= count) { node = cancel; return 0; }
-            if(COUNT) { cnt.visits++; if(axis < 0) cnt.tlas_visits++; }
-            accept = __float_as_uint(lo2.w);
-            cancel = __float_as_uint(hi2.w);
-            if(!box_hit(lo2, hi2)) { node = cancel; return 0; }
-#else
-            node = cancel;
-            return 0;
-#endif
+            const uint32_t tested = !(a0 & kBeNone) + !(a1 & kBeNone) + !(a2 & kBeNone) + !(a3 & kBeNone);
+            cnt.visits += tested;
+            if(axis < 0) cnt.tlas_visits += tested;
         }
-        if(!(accept & 0x80000000u)) { node = accept; return 0; }
-        node = cancel;
-        const uint32_t leaf = accept & 0x7FFFFFFFu;
+        const uint32_t hits = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
+        // passing entries in the ray's order: bit j = the entry met j-th
+        const uint32_t om = ((hits >> (perm & 3u)) & 1u) | (((hits >> ((perm >> 4) & 3u)) & 1u) << 1) |
+                            (((hits >> ((perm >> 8) & 3u)) & 1u) << 2) | (((hits >> ((perm >> 12) & 3u)) & 1u) << 3);
+        // slot t's word / near: two selects on t's bits (no branches)
+        const uint32_t m0 = __float_as_uint(n0), m1 = __float_as_uint(n1), m2 = __float_as_uint(n2),
+                       m3 = __float_as_uint(n3);
+        auto slot_a = [=](uint32_t t) { return sel4(t, a0, a1, a2, a3); };
+        auto slot_n = [=](uint32_t t) { return sel4(t, m0, m1, m2, m3); };
+        // the first is walked next; the others are pushed last-first, so they
+        // pop in the ray's order
+        const uint32_t first = (perm >> (4u * uint32_t(__builtin_ctz(om | 16u)))) & 3u;
+        cur = om ? slot_a(first) : kBePop;
+        const uint32_t rest = om & (om - 1u);
+        if(rest)
+        {
+            st.reserve(kBlockWidth - 1);
+            uint32_t k = 0;
+#pragma unroll
+            for(uint32_t j = kBlockWidth - 1; j >= 1; --j)
+            {   // written into the reserved room either way, kept only if pushed
+                const uint32_t t = (perm >> (4u * j)) & 3u;
+                st.put(k, make_uint2(slot_a(t), slot_n(t)));
+                k += (rest >> j) & 1u;
+            }
+            st.advance(k);
+        }
+        return 0;
+    }
+
+    // Leaf phase: the triangle test, or the BLAS entry, the walk stands at.
+    // Returns 0, or 2 (ANY only) when the triangle occludes the ray.
+    template<bool ANY, bool COUNT>
+    PTG_D int leaf_step(const DevScene& sc, Counters& cnt)
+    {
+        const uint32_t id = cur & kBeIndex;
+        cur = kBePop;
         if(axis < 0)
         {
-            PTG_CHECK(sc, leaf < sc.inst_count, kDebugInst);
+            PTG_CHECK(sc, id < sc.inst_count, kDebugInst);
             if(COUNT) { cnt.blas_entries++; cnt.step_loads |= 4u; }
             // whole-row vector loads: float4 members get re-split by the
             // compiler into unaligned pieces (5 loads instead of 4)
-            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + leaf);
-            enter(leaf, ip[0], ip[1], ip[2], ip[3]);
+            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + id);
+            enter(id, ip[0], ip[1], ip[2], ip[3]);
             return 0;
         }
         if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
-        PTG_CHECK(sc, tri_base + leaf < sc.tri_count, kDebugTri);
-        const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + leaf);
-        return tri_test<ANY>(leaf, tp[0], tp[1], tp[2]);
+        PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
+        const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + id);
+        return tri_test<ANY>(id, tp[0], tp[1], tp[2]);
+    }
+
+    // One step of either phase (the per-lane walks: the megakernel and the
+    // per-ray entry points).  Returns 0 while the walk goes on, 1 when it
+    // has ended, 2 (ANY only) when an occluder was found.
+    template<bool ANY, bool COUNT>
+    PTG_D int step(const DevScene& sc, Counters& cnt)
+    {
+        if(at_leaf()) return leaf_step<ANY, COUNT>(sc, cnt);
+        return node_step<COUNT>(sc, cnt);
     }
 };
 
-using Walker = WalkerT<RegCold>;
+using Walker = BlockWalker<RegCold, PrivStack>;
 
 // A whole query on one lane.  Returns whether the ray hit (ANY: occluded).
+// `root` is the TLAS's root block (tlas_of), `unused` keeps the reference
+// layout's (count, offset) call shape.
 template<bool ANY, bool COUNT>
-PTG_D bool trace(const DevScene& sc, uint32_t tlas_count, uint32_t tlas_offset, f3 o, f3 d, float tmin, float tmax,
-                 Hit& best, Counters& cnt)
+PTG_D bool trace(const DevScene& sc, uint32_t root, uint32_t /*unused*/, f3 o, f3 d, float tmin, float tmax, Hit& best,
+                 Counters& cnt)
 {
     if(COUNT) cnt.queries++;
     Walker w;
-    w.init(sc, tlas_count, tlas_offset, o, d, tmin, tmax);
+    w.init(root, o, d, tmin, tmax);
     int r;
     while((r = w.template step<ANY, COUNT>(sc, cnt)) == 0) {}
     best = w.result();
@@ -1088,6 +1245,20 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
     info.roughness = 1.0f - (1.0f - info.roughness) * regularization;
 }
 
+// A subframe's TLAS handle in the form the scene's trace() takes: the root
+// block of its packed TLAS (DevScene), or the reference's (node_count,
+// node_offset) pair (RefScene, scene.hh:26-34).
+PTG_D void tlas_of(const DevScene& sc, const uint8_t* sf, uint32_t& a, uint32_t& b)
+{
+    a = sc.tlas_root[uint32_t(sf - sc.subframes) / SF_STRIDE];
+    b = 0;
+}
+PTG_D void tlas_of(const RefScene&, const uint8_t* sf, uint32_t& a, uint32_t& b)
+{
+    a = rd_u(sf, SF_TLAS);
+    b = rd_u(sf, SF_TLAS + 4);
+}
+
 // path_trace_pixel (path_tracer.hh:637-741) as one device function (used by
 // the per-sample entry point; the frame renderer runs the same steps as a
 // wavefront pipeline, csrc/device/wavefront.h).
@@ -1095,7 +1266,8 @@ template<bool COUNT, class SC>
 PTG_D f3 path_trace_sample(const SC& sc, uint32_t px, uint32_t py, int32_t sample_index, Counters& cnt)
 {
     const uint8_t* sf = subframe_of(sc, sample_index);
-    const uint32_t tc = rd_u(sf, SF_TLAS), to = rd_u(sf, SF_TLAS + 4);
+    uint32_t tc, to;
+    tlas_of(sc, sf, tc, to);
     const Light L = light_of(sf);
     u4 seed;
     f3 ray_o, ray_dir;

@@ -1,0 +1,348 @@
+// Block BVH packer (device/block_format.h): the reference's nodes and eight
+// link orders (bvh.cc:145-229) -> 4-wide blocks, breadth-first, so the top
+// levels every ray walks share cache lines.
+#include "block_bvh.h"
+#include <algorithm>
+#include <cmath>
+#include <limits>
+
+namespace ptg {
+
+namespace {
+
+struct Tree {
+    std::vector<std::vector<uint32_t>> kids;   // children in build (forward) order
+    std::vector<uint32_t> axis;                // split / sort axis (orders the children)
+    std::vector<uint32_t> payload;             // leaves: kBeLeaf | payload, else 0
+    std::vector<ptg_bvh_node> box;
+    bool leaf(uint32_t n) const { return (payload[n] & kBeLeaf) != 0; }
+};
+
+bool contains(const ptg_bvh_node& p, const ptg_bvh_node& c)
+{
+    return p.min_x <= c.min_x && p.min_y <= c.min_y && p.min_z <= c.min_z && c.max_x <= p.max_x && c.max_y <= p.max_y &&
+           c.max_z <= p.max_z;
+}
+
+double area(const ptg_bvh_node& b)
+{
+    const double x = double(b.max_x) - b.min_x, y = double(b.max_y) - b.min_y, z = double(b.max_z) - b.min_z;
+    return x * y + y * z + z * x;
+}
+
+// The tree behind the links, checked against the reference builder's rules.
+bool derive(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t payload_limit, Tree& t,
+            std::string& err)
+{
+    auto L = [&](uint32_t o, uint32_t i) -> const ptg_bvh_link& { return links[size_t(o) * count + i]; };
+    t.kids.assign(count, {});
+    t.axis.assign(count, 0);
+    t.payload.assign(count, 0);
+    t.box.assign(nodes, nodes + count);
+    std::vector<uint8_t> parents(count, 0);
+    for(uint32_t n = 0; n < count; ++n)
+    {
+        const ptg_bvh_link& l7 = L(7, n);   // order 7: every sign positive, nothing reversed (bvh.cc:178)
+        if(l7.accept & 0x80000000u)
+        {
+            const uint32_t p = l7.accept & 0x7FFFFFFFu;
+            if(p >= payload_limit || p > kBeIndex)
+            {
+                err = "leaf payload " + std::to_string(p) + " out of range (limit " + std::to_string(payload_limit) + ")";
+                return false;
+            }
+            for(uint32_t o = 0; o < 8; ++o)
+                if(L(o, n).accept != l7.accept) { err = "leaf payload differs between link orders"; return false; }
+            t.payload[n] = kBeLeaf | p;
+            continue;
+        }
+        uint32_t c = l7.accept;
+        for(;;)
+        {
+            if(c >= count || c == 0) { err = "link outside the BVH"; return false; }
+            if(parents[c]++) { err = "node with two parents"; return false; }
+            t.kids[n].push_back(c);
+            const uint32_t nx = L(7, c).cancel;
+            if(nx == l7.cancel) break;
+            c = nx;
+        }
+        const std::vector<uint32_t>& k = t.kids[n];
+        bool found = k.size() < 2;   // one child: the order is moot
+        for(uint32_t a = 0; a < 3 && !found; ++a)
+            if(L(1u << a, n).accept == k[0]) { t.axis[n] = a; found = true; }
+        if(!found) { err = "child order matches no axis"; return false; }
+        for(uint32_t o = 0; o < 8; ++o)
+        {
+            const bool rev = ((o >> t.axis[n]) & 1u) == 0;
+            auto child = [&](size_t j) { return k[rev ? k.size() - 1 - j : j]; };
+            if(L(o, n).accept != child(0)) { err = "accept link is not the first child of its order"; return false; }
+            for(size_t j = 0; j < k.size(); ++j)
+                if(L(o, child(j)).cancel != (j + 1 < k.size() ? child(j + 1) : L(o, n).cancel))
+                { err = "cancel link breaks the child order"; return false; }
+        }
+        for(uint32_t ch: k)
+            if(!contains(t.box[n], t.box[ch])) { err = "box does not contain its child's box"; return false; }
+    }
+    for(uint32_t n = 1; n < count; ++n)
+        if(!parents[n]) { err = "node not reachable from the root"; return false; }
+    for(uint32_t o = 0; o < 8; ++o)
+        if(L(o, 0).cancel < count) { err = "root has a successor"; return false; }
+    return true;
+}
+
+// Nodes with more than kBlockWidth children (multi-leaf buckets) get
+// consecutive runs of their children grouped under virtual nodes with the
+// same axis and the union box: the order rule, and containment, carry over.
+void split_wide(Tree& t)
+{
+    const size_t W = kBlockWidth;
+    for(uint32_t n = 0; n < t.kids.size(); ++n)
+    {
+        while(t.kids[n].size() > W)
+        {
+            const std::vector<uint32_t> ks = t.kids[n];
+            const size_t groups = (ks.size() + W - 1) / W;
+            std::vector<uint32_t> out;
+            for(size_t i = 0, g = 0; i < ks.size(); ++g)
+            {
+                const size_t take = std::min(W, (ks.size() - i + (groups - g) - 1) / (groups - g));
+                if(take == 1) { out.push_back(ks[i++]); continue; }
+                ptg_bvh_node b = t.box[ks[i]];
+                for(size_t j = i + 1; j < i + take; ++j)
+                {
+                    const ptg_bvh_node& c = t.box[ks[j]];
+                    b.min_x = std::min(b.min_x, c.min_x); b.min_y = std::min(b.min_y, c.min_y); b.min_z = std::min(b.min_z, c.min_z);
+                    b.max_x = std::max(b.max_x, c.max_x); b.max_y = std::max(b.max_y, c.max_y); b.max_z = std::max(b.max_z, c.max_z);
+                }
+                const uint32_t v = uint32_t(t.kids.size());
+                t.kids.emplace_back(ks.begin() + i, ks.begin() + i + take);
+                t.axis.push_back(t.axis[n]);
+                t.payload.push_back(0);
+                t.box.push_back(b);
+                out.push_back(v);
+                i += take;
+            }
+            t.kids[n] = out;
+        }
+    }
+}
+
+BlockEntry none_entry()
+{
+    const float q = std::numeric_limits<float>::quiet_NaN();
+    BlockEntry e;
+    e.lo_x = e.lo_y = e.lo_z = e.hi_x = e.hi_y = e.hi_z = q;
+    e.a = kBeNone;
+    e.b = 0;
+    return e;
+}
+
+} // namespace
+
+bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t block_base,
+                    uint32_t payload_limit, std::vector<BlockEntry>& out, BlockBvh& info, std::string& err)
+{
+    if(count == 0) { err = "empty BVH"; return false; }
+    Tree t;
+    if(!derive(nodes, links, count, payload_limit, t, err)) return false;
+    split_wide(t);
+    const uint32_t W = kBlockWidth;
+
+    // Block contents: a block root's children, greedily replacing the inner
+    // slot with the largest surface area by its own children while they fit.
+    struct Blk {
+        uint32_t root;
+        std::vector<uint32_t> slots, expanded;
+    };
+    std::vector<Blk> blks;
+    std::vector<uint32_t> block_of(t.kids.size(), 0);
+    auto make = [&](uint32_t root) {
+        Blk b;
+        b.root = root;
+        b.slots = t.kids[root];
+        b.expanded.push_back(root);
+        for(;;)
+        {
+            int best = -1;
+            double ba = -1.0;
+            for(size_t i = 0; i < b.slots.size(); ++i)
+            {
+                const uint32_t c = b.slots[i];
+                if(t.leaf(c) || b.slots.size() - 1 + t.kids[c].size() > W) continue;
+                const double a = area(t.box[c]);
+                if(a > ba) { ba = a; best = int(i); }
+            }
+            if(best < 0) break;
+            const uint32_t c = b.slots[size_t(best)];
+            b.expanded.push_back(c);
+            b.slots.erase(b.slots.begin() + best);
+            b.slots.insert(b.slots.begin() + best, t.kids[c].begin(), t.kids[c].end());
+        }
+        return b;
+    };
+    if(t.leaf(0))
+    {   // a one-leaf BVH: its block holds the leaf
+        Blk b;
+        b.root = 0;
+        b.slots.push_back(0);
+        blks.push_back(b);
+    }
+    else
+        blks.push_back(make(0));
+    for(size_t q = 0; q < blks.size(); ++q)            // breadth-first
+    {
+        block_of[blks[q].root] = block_base + uint32_t(out.size() / W + q);
+        for(uint32_t c: std::vector<uint32_t>(blks[q].slots))
+            if(!t.leaf(c)) blks.push_back(make(c));
+    }
+    if(uint64_t(block_base) + out.size() / W + blks.size() > kBeIndex) { err = "BVH records above 2^28 blocks"; return false; }
+    if(out.size() % W) { err = "unaligned block output"; return false; }
+
+    // stack bound: a block step walks one passing entry and pushes the
+    // others (at most all but one); a walk holds at most one block's pushes
+    // per level of its path
+    std::vector<uint32_t> bound(blks.size(), 0);
+    const uint32_t first = uint32_t(out.size() / W) + block_base;
+    for(size_t q = blks.size(); q-- > 0;)
+    {
+        uint32_t own = uint32_t(blks[q].slots.size()) - 1u, below = 0;
+        for(uint32_t c: blks[q].slots)
+        {
+            if(!t.leaf(c)) below = std::max(below, bound[block_of[c] - first]);   // children come later (BFS)
+        }
+        bound[q] = own + below;
+    }
+
+    for(const Blk& b: blks)
+    {
+        BlockEntry e[kBlockWidth];
+        for(uint32_t s = 0; s < W; ++s)
+        {
+            if(s >= b.slots.size()) { e[s] = none_entry(); continue; }
+            const uint32_t c = b.slots[s];
+            const ptg_bvh_node& n = t.box[c];
+            e[s].lo_x = n.min_x; e[s].lo_y = n.min_y; e[s].lo_z = n.min_z;
+            e[s].hi_x = n.max_x; e[s].hi_y = n.max_y; e[s].hi_z = n.max_z;
+            e[s].a = t.leaf(c) ? t.payload[c] : block_of[c];
+            e[s].b = 0;
+        }
+        // slot order per octant: depth-first through the expanded nodes, each
+        // one's children forward or reversed by its axis (bvh.cc:177-181)
+        for(uint32_t o = 0; o < 8; ++o)
+        {
+            std::vector<uint32_t> seq;
+            auto walk = [&](auto&& self, uint32_t n) -> void {
+                const std::vector<uint32_t>& ks = t.kids[n];
+                const bool rev = ((o >> t.axis[n]) & 1u) == 0;
+                for(size_t j = 0; j < ks.size(); ++j)
+                {
+                    const uint32_t c = ks[rev ? ks.size() - 1 - j : j];
+                    if(std::find(b.expanded.begin(), b.expanded.end(), c) != b.expanded.end()) self(self, c);
+                    else seq.push_back(uint32_t(std::find(b.slots.begin(), b.slots.end(), c) - b.slots.begin()));
+                }
+            };
+            if(t.leaf(b.root)) seq.push_back(0);
+            else walk(walk, b.root);
+            uint32_t p = 0;
+            for(uint32_t j = 0; j < W; ++j) p |= (j < seq.size() ? seq[j] : j) << (4 * j);
+            e[o >> 1].b |= p << (16 * (o & 1));
+        }
+        for(uint32_t s = 0; s < W; ++s) out.push_back(e[s]);
+    }
+    info.root = block_base + uint32_t((out.size() / W) - blks.size());
+    info.blocks = uint32_t(blks.size());
+    info.stack_entries = bound.empty() ? 0 : bound[0];
+    info.max_payload = 0;
+    for(uint32_t n = 0; n < count; ++n)
+        if(t.leaf(n)) info.max_payload = std::max(info.max_payload, t.payload[n] & kBeIndex);
+    return true;
+}
+
+} // namespace ptg
+
+namespace ptg {
+
+int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link* static_links, size_t static_count,
+                           size_t index_count, size_t vertex_count, const ptg_subframe* subframes, size_t subframe_count,
+                           const ptg_tlas_instance* instances, size_t instance_count, const ptg_bvh_node* frame_nodes,
+                           const ptg_bvh_link* frame_links, size_t first_node, size_t frame_node_count, FramePack& fp,
+                           std::string& err) const
+{
+    const uint32_t W = kBlockWidth;
+    fp = FramePack();
+    fp.blas_base = uint32_t(blas.size() / W);
+    fp.blas_stack = blas_stack;
+    fp.inst_root.resize(instance_count);
+    std::string why;
+    for(size_t i = 0; i < instance_count; ++i)
+    {
+        const ptg_tlas_instance& in = instances[i];
+        const std::string who = "instance " + std::to_string(i);
+        if(uint64_t(in.blas.node_offset) + in.blas.node_count > static_count || in.blas.node_count == 0)
+        { err = who + ": BLAS outside the static nodes"; return PTG_E_RANGE; }
+        if(uint64_t(in.m.index_offset) + 3ull * in.m.triangle_count > index_count || in.m.index_offset % 3 ||
+           uint64_t(in.m.base_vertex_offset) + in.m.vertex_count > vertex_count)
+        { err = who + ": mesh outside the uploaded buffers"; return PTG_E_RANGE; }
+        const uint32_t key = in.blas.node_offset;
+        BlasRecord rec;
+        if(auto o = records.find(key); o != records.end()) rec = o->second;
+        else if(auto f = fp.new_records.find(key); f != fp.new_records.end()) rec = f->second;
+        else
+        {
+            BlockBvh info;
+            if(!pack_block_bvh(static_nodes + in.blas.node_offset, static_links + size_t(in.blas.node_offset) * 8,
+                               in.blas.node_count, fp.blas_base, 1u << 28, fp.new_blas, info, why))
+            { err = who + ": BLAS at node " + std::to_string(in.blas.node_offset) + ": " + why; return PTG_E_RANGE; }
+            rec.root = info.root;
+            rec.count = in.blas.node_count;
+            rec.max_payload = info.max_payload;
+            fp.new_records[key] = rec;
+            fp.blas_stack = std::max(fp.blas_stack, info.stack_entries);
+        }
+        if(rec.count != in.blas.node_count) { err = who + ": BLAS node count differs from an earlier instance's"; return PTG_E_RANGE; }
+        if(rec.max_payload >= in.m.triangle_count)
+        {
+            err = who + ": BLAS names triangle " + std::to_string(rec.max_payload) + " of a " +
+                  std::to_string(in.m.triangle_count) + "-triangle mesh";
+            return PTG_E_RANGE;
+        }
+        fp.inst_root[i] = rec.root;
+    }
+    fp.tlas_base = fp.blas_base + uint32_t(fp.new_blas.size() / W);
+    fp.tlas_root.resize(subframe_count);
+    for(size_t i = 0; i < subframe_count; ++i)
+    {
+        const ptg_bvh& t = subframes[i].tlas;
+        if(t.node_offset < first_node || uint64_t(t.node_offset) + t.node_count > first_node + frame_node_count ||
+           t.node_count == 0)
+        { err = "subframe " + std::to_string(i) + ": TLAS outside the frame nodes"; return PTG_E_RANGE; }
+        const size_t rel = t.node_offset - first_node;
+        BlockBvh info;
+        // every TLAS leaf must name a valid instance
+        if(!pack_block_bvh(frame_nodes + rel, frame_links + 8 * rel, t.node_count, fp.tlas_base, uint32_t(instance_count),
+                           fp.tlas, info, why))
+        { err = "subframe " + std::to_string(i) + ": TLAS: " + why; return PTG_E_RANGE; }
+        fp.tlas_root[i] = info.root;
+        fp.tlas_stack = std::max(fp.tlas_stack, info.stack_entries);
+    }
+    // every block index a walk can follow lies inside the buffer (the
+    // committed BLAS blocks were checked when they were added)
+    const uint32_t total = fp.total_blocks();
+    for(const std::vector<BlockEntry>* v: {&fp.new_blas, &fp.tlas})
+        for(const BlockEntry& e: *v)
+            if(!(e.a & (kBeLeaf | kBeNone)) && e.a >= total) { err = "block link outside the block buffer"; return PTG_E_RANGE; }
+    for(uint32_t r: fp.tlas_root)
+        if(r >= total) { err = "TLAS root outside the block buffer"; return PTG_E_RANGE; }
+    for(uint32_t r: fp.inst_root)
+        if(r >= total) { err = "BLAS root outside the block buffer"; return PTG_E_RANGE; }
+    return PTG_OK;
+}
+
+void BlockCache::commit(FramePack& fp)
+{
+    blas.insert(blas.end(), fp.new_blas.begin(), fp.new_blas.end());
+    for(const auto& kv: fp.new_records) records[kv.first] = kv.second;
+    blas_stack = fp.blas_stack;
+}
+
+} // namespace ptg

@@ -1,7 +1,7 @@
 // HIP kernels + C ABI of the GPU renderer (include/ptg.h).
 //
-//   k_pack_bvh      reference nodes + 8 link orders -> TravRec (32 B / visit)
 //   k_pack_tris     indices + positions -> TriRec (48 B / triangle)
+//   (BVH blocks are packed on the host, host/block_bvh.cpp)
 //   k_trace         path_trace_pixel for a (pixel set x sample chunk) grid,
 //                   one work-item per (pixel, sample); results to a
 //                   [sample][pixel] float4 buffer in HBM
@@ -25,7 +25,9 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include <unordered_map>
 #include <unordered_set>
+#include "host/block_bvh.h"
 #include <vector>
 
 namespace ptg {
@@ -43,77 +45,6 @@ constexpr int kBlock = 256;
 #endif
 
 // ---------------------------------------------------------------- kernels --
-
-struct BvhJob {
-    uint32_t node_begin;   // first node in the raw node array
-    uint32_t link_begin;   // first link in the raw link array (8 orders follow)
-    uint32_t count;        // nodes in this BVH
-    uint32_t out_begin;    // first record in the output TravRec array
-};
-
-// Depth-first record order.  The walk visits nodes in each link order's
-// pre-order (accept = first child, cancel = next subtree), so each order's
-// records are stored in that order: after a hit the next node is the very next
-// record (same cache line), after a miss the walk jumps forward.  Node
-// identities, boxes and the link structure are unchanged - only addresses.
-// perm[link index] = position of the node in its order's pre-order walk
-// (0xFFFFFFFF for a node the walk cannot reach).  One thread per (BVH, order).
-constexpr uint32_t kUnreached = 0xFFFFFFFFu;
-
-__global__ void k_preorder(const ptg_bvh_link* __restrict__ links, uint32_t* __restrict__ perm,
-                           const BvhJob* __restrict__ jobs, uint32_t njobs)
-{
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if(t >= 8u * njobs) return;
-    const BvhJob j = jobs[t / 8u];
-    const uint32_t base = j.link_begin + (t % 8u) * j.count;
-    uint32_t n = 0, pos = 0;
-    while(n < j.count && pos < j.count)
-    {
-        perm[base + n] = pos++;
-        const ptg_bvh_link l = links[base + n];
-        n = (l.accept & 0x80000000u) ? l.cancel : l.accept;
-    }
-}
-
-__global__ void k_pack_bvh(const ptg_bvh_node* __restrict__ nodes, const ptg_bvh_link* __restrict__ links,
-                           const uint32_t* __restrict__ perm, TravRec* __restrict__ out, const BvhJob* __restrict__ jobs)
-{
-    const BvhJob j = jobs[blockIdx.y];
-    const uint32_t total = 8u * j.count;
-    for(uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x)
-    {
-        const uint32_t i = k % j.count, ob = k - i;     // node, first link of its order
-        const uint32_t p = perm[j.link_begin + k];
-        if(p == kUnreached) continue;
-        const uint32_t* pm = perm + j.link_begin + ob;
-        const ptg_bvh_node n = nodes[j.node_begin + i];
-        const ptg_bvh_link l = links[j.link_begin + k];
-        TravRec r;
-        r.min_x = n.min_x; r.min_y = n.min_y; r.min_z = n.min_z;
-        r.accept = (l.accept & 0x80000000u) ? l.accept : pm[l.accept];
-        r.max_x = n.max_x; r.max_y = n.max_y; r.max_z = n.max_z;
-        r.cancel = l.cancel < j.count ? pm[l.cancel] : l.cancel;
-#if PTG_PAIR_NODES
-        if(l.cancel < j.count)
-        {
-            const uint32_t c = l.cancel;
-            const ptg_bvh_node n2 = nodes[j.node_begin + c];
-            const ptg_bvh_link l2 = links[j.link_begin + ob + c];   // same link order
-            r.min2_x = n2.min_x; r.min2_y = n2.min_y; r.min2_z = n2.min_z;
-            r.accept2 = (l2.accept & 0x80000000u) ? l2.accept : pm[l2.accept];
-            r.max2_x = n2.max_x; r.max2_y = n2.max_y; r.max2_z = n2.max_z;
-            r.cancel2 = l2.cancel < j.count ? pm[l2.cancel] : l2.cancel;
-        }
-        else
-        {
-            r.min2_x = r.min2_y = r.min2_z = 0.0f; r.accept2 = 0xFFFFFFFFu;
-            r.max2_x = r.max2_y = r.max2_z = 0.0f; r.cancel2 = 0xFFFFFFFFu;
-        }
-#endif
-        out[j.out_begin + ob + p] = r;
-    }
-}
 
 // The aperture polygon's vertex directions of every subframe (regular_polygon,
 // path_tracer.hh:50-62): (sin, cos) of side_radians * k + angle for
@@ -249,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
         if(!live)
         {
             if(in_chunk) st_out(out + slot, make_float4(0.f, 0.f, 0.f, 0.f));
-            st_state(S.meta + i, make_uint4(slot, META_DEAD, 0u, 0u));
+            st_state(S.meta + i, make_uint4(slot, META_DEAD, kBePop, 0u));   // no TLAS: the walk ends at once
             st_state(S.ray_o + i, make_float4(0.f, 0.f, 0.f, 0.f));
             st_state(S.ray_d + i, make_float4(0.f, 0.f, 1.f, 0.f));
             continue;
@@ -259,8 +190,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
         u4 seed;
         f3 o, d;
         camera_ray(sc, sf, x, y, j, seed, o, d);
-        st_state(S.meta + i, make_uint4(slot, meta_pack(0, false, (uint32_t)(sf - sc.subframes) / SF_STRIDE),
-                                        rd_u(sf, SF_TLAS), rd_u(sf, SF_TLAS + 4)));
+        const uint32_t sub = (uint32_t)(sf - sc.subframes) / SF_STRIDE;
+        st_state(S.meta + i, make_uint4(slot, meta_pack(0, false, sub), sc.tlas_root[sub], 0u));
         st_state(S.seed + i, to_uint4(seed));
         st_state(S.ray_o + i, make_float4(o.x, o.y, o.z, 0.f));
         st_state(S.ray_d + i, make_float4(d.x, d.y, d.z, 0.f));
@@ -285,16 +216,16 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #define PTG_WALK_ATTR
 #endif
 #ifndef PTG_WALK_UNROLL
-#define PTG_WALK_UNROLL 3   // walk steps per refill check (measured with the LDS walker: 3 beats 2 by 0.3-0.5%, 1 is slower)
-#endif
-#ifndef PTG_WALK_LDS
-#define PTG_WALK_LDS 1
+#define PTG_WALK_UNROLL 2   // node steps per leaf phase (block walker, 256 spp: 2 beats 1 by 1-3% and 3 by 2-5%, 4 is slower)
 #endif
 #ifndef PTG_VMEM_STATS
 #define PTG_VMEM_STATS 0
 #endif
 #ifndef PTG_WF_SLOTS
 #define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
+#endif
+#ifndef PTG_WALK_RESIDENT
+#define PTG_WALK_RESIDENT 5 // walk blocks per CU (LDS-bound with 12-entry stack rings: 5 x 32 KB)
 #endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
@@ -325,17 +256,37 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
-#if PTG_WALK_LDS
-    // the walk's cold state in LDS: 64 VGPRs instead of 76, so a sky wave
-    // fits beside six walk waves on a SIMD (see ptg_context_create)
+    // LDS: every lane's world ray, then the stack rings, one 64-lane x kRing
+    // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
-    WalkerT<LdsCold> w;
-    w.cold.c = &cold[threadIdx.x];
-#else
-    Walker w;
-#endif
+    BlockWalker<LdsCold, LdsStack> w;
+    w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C casts: generic -> LDS address space
+    w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kRing) + lane);
+    w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
     bool active = false;
     uint32_t q = 0;
+    // a finished walk writes its result: the shadow flag, or the closest hit
+    auto finish = [&](int r) {
+#if PTG_NT_STATE
+        if(ANY) __builtin_nontemporal_store(r == 2 ? 1u : 0u, tr.shadow + q);
+#else
+        if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
+#endif
+        else
+        {
+            const Hit h = w.result();
+#if PTG_NT_STATE
+            nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
+#if PTG_MISS_BARY
+            if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
+#endif
+                nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
+#else
+            tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
+            tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
+#endif
+        }
+    };
 #if PTG_VMEM_STATS
     uint32_t vm_rec = 0, vm_tri = 0, vm_inst = 0, vm_refill = 0;
 #endif
@@ -369,11 +320,11 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                             // path state streams once through the caches: non-temporal, so it
                             // does not evict BVH records from L2 / the Infinity Cache
                             const uint4 m = nt_load(S.meta + q);
-                            w.init(sc, m.z, m.w, xyz(nt_load(S.ray_o + q)),
+                            w.init(m.z, xyz(nt_load(S.ray_o + q)),
                                    ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)), tmin, tmax);
 #else
                             const uint4 m = S.meta[q];
-                            w.init(sc, m.z, m.w, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
+                            w.init(m.z, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
 #endif
                             active = true;
                             if(COUNT) cnt.queries++;
@@ -385,51 +336,42 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
         }
         if(!__any(active)) break;
         if(COUNT && lane == 0) cnt.iters++;   // wave loop iterations (lane 0 counts for its wave)
+        // Node phase, up to PTG_WALK_UNROLL block steps (each after the pop it
+        // needs), for lanes not standing at a leaf; then one leaf phase for the
+        // lanes that are.  The leaf code (triangle test, BLAS entry) then runs
+        // once per iteration with many lanes, not once per block step with few.
+        int r = 0;
 #pragma unroll
         for(int u = 0; u < PTG_WALK_UNROLL; ++u)
         {
 #if PTG_VMEM_STATS
-        // diagnostic build: wave-level load instructions of each step by kind,
-        // counted in the walk kinds' unused slots: [0] record, [5] triangle,
-        // [6] instance, [7] refill (see tools/ablate.py --counters)
+            if(COUNT) cnt.step_loads = 0;
+#endif
+            if(active && !w.at_leaf()) r = w.template node_step<COUNT>(sc, cnt);
+#if PTG_VMEM_STATS
+            if(COUNT)
+            {
+                const unsigned long long br = __ballot(cnt.step_loads & 1u);
+                if(lane == 0) vm_rec += br != 0;
+            }
+#endif
+            if(active && r != 0) { finish(r); active = false; r = 0; }
+        }
+#if PTG_VMEM_STATS
         if(COUNT) cnt.step_loads = 0;
 #endif
-        if(active)
+        if(active && w.at_leaf())
         {
-            const int r = w.template step<ANY, COUNT>(sc, cnt);
-            if(r != 0)
-            {
-#if PTG_NT_STATE
-                if(ANY) __builtin_nontemporal_store(r == 2 ? 1u : 0u, tr.shadow + q);
-#else
-                if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
-#endif
-                else
-                {
-                    const Hit h = w.result();
-#if PTG_NT_STATE
-                    nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
-#if PTG_MISS_BARY
-                    if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
-#endif
-                        nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
-#else
-                    tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
-                    tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
-#endif
-                }
-                active = false;
-            }
+            r = w.template leaf_step<ANY, COUNT>(sc, cnt);
+            if(r != 0) { finish(r); active = false; }
         }
 #if PTG_VMEM_STATS
         if(COUNT)
         {
-            const unsigned long long br = __ballot(cnt.step_loads & 1u), bt = __ballot(cnt.step_loads & 2u),
-                                     bi = __ballot(cnt.step_loads & 4u);
-            if(lane == 0) { vm_rec += br != 0; vm_tri += bt != 0; vm_inst += bi != 0; }
+            const unsigned long long bt = __ballot(cnt.step_loads & 2u), bi = __ballot(cnt.step_loads & 4u);
+            if(lane == 0) { vm_tri += bt != 0; vm_inst += bi != 0; }
         }
 #endif
-        }
     }
 #if PTG_VMEM_STATS
     if(COUNT) { cnt.shades = vm_tri; cnt.tlas_visits = vm_inst; cnt.iters = vm_refill; }
@@ -705,7 +647,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_list(DevScene sc, uint32_t n,
     out[i] = make_float4(c.x, c.y, c.z, 0.f);
 }
 
-__global__ __launch_bounds__(kBlock) void k_rays(DevScene sc, uint32_t tlas_count, uint32_t tlas_offset, uint32_t n,
+__global__ __launch_bounds__(kBlock) void k_rays(DevScene sc, uint32_t tlas_root, uint32_t n,
                                                  const float* __restrict__ rays, uint32_t* __restrict__ hits)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -714,8 +656,8 @@ __global__ __launch_bounds__(kBlock) void k_rays(DevScene sc, uint32_t tlas_coun
     const f3 o = V3(r[0], r[1], r[2]), d = V3(r[3], r[4], r[5]);
     Counters cnt;
     Hit h, unused;
-    trace<false, false>(sc, tlas_count, tlas_offset, o, d, r[6], r[7], h, cnt);
-    const bool shadow = trace<true, false>(sc, tlas_count, tlas_offset, o, d, r[6], r[7], unused, cnt);
+    trace<false, false>(sc, tlas_root, 0, o, d, r[6], r[7], h, cnt);
+    const bool shadow = trace<true, false>(sc, tlas_root, 0, o, d, r[6], r[7], unused, cnt);
     uint32_t* w = hits + size_t(i) * 8;
     w[0] = __float_as_uint(h.bx);
     w[1] = __float_as_uint(h.by);
@@ -785,15 +727,23 @@ struct ptg_context {
     int device = 0;
     hipStream_t stream = nullptr;
     bool counting = false;
-    // static scene (reference layout) + repacked records
-    DevBuf nodes, links, indices, pos, normal, albedo, material;
-    DevBuf trav, tris, perm;   // trav: BLAS records then the frame's TLAS records, by global link index
+    // static scene: the shading arrays in reference layout, the triangle
+    // records, and a host copy of the BLAS nodes + links (packed into blocks
+    // when an instance first names a BLAS)
+    DevBuf indices, pos, normal, albedo, material, tris;
+    std::vector<ptg_bvh_node> host_nodes;
+    std::vector<ptg_bvh_link> host_links;
     size_t static_nodes = 0, index_count = 0, vertex_count = 0;
-    std::unordered_set<uint32_t> packed_bvh, packed_mesh;
+    std::unordered_set<uint32_t> packed_mesh;
+    // BLAS blocks packed so far (host copy; their device copy leads `blocks`)
+    BlockCache cache;
+    size_t blas_on_device = 0;                           // leading cache.blas entries already in `blocks`
     bool scene_ready = false;
-    // frame
-    DevBuf frame_nodes, frame_links, subframes, inst_trav, inst_shade, jobs, polygon;
-    size_t first_frame_node = 0, frame_node_count = 0, subframe_count = 0, instance_count = 0;
+    // frame: blocks = [BLAS blocks][this frame's TLAS blocks]
+    DevBuf blocks, tlas_root, subframes, inst_trav, inst_shade, jobs, polygon, spill;
+    size_t block_count = 0, subframe_count = 0, instance_count = 0;
+    uint32_t stack_bound = 0;                            // TLAS + BLAS stack bound of this frame (entries)
+    std::vector<uint32_t> host_tlas_root;
     std::vector<ptg_subframe> host_subframes;
     bool frame_ready = false;
     // render workspace
@@ -810,7 +760,7 @@ struct ptg_context {
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
-    uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state, padded to cap residency
+    uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
     uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (PTG_HBM_PCT)
     // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2).  2^27
     // paths x 392 B = 53 GB per pipeline, ~37% of an MI355X's HBM for the two
@@ -866,7 +816,8 @@ struct ptg_context {
     DevScene scene_args(const ptg_render_config* cfg) const
     {
         DevScene s;
-        s.trav = trav.as<TravRec>();
+        s.blocks = blocks.as<BlockEntry>();
+        s.tlas_root = tlas_root.as<uint32_t>();
         s.tris = tris.as<TriRec>();
         s.inst_trav = inst_trav.as<InstTrav>();
         s.inst_shade = inst_shade.as<InstShade>();
@@ -883,7 +834,9 @@ struct ptg_context {
         s.student_id = cfg ? cfg->student_id : 0;
         s.blur_step = cfg ? cfg->samples_per_motion_blur_step : 8;
         s.subframe_count = uint32_t(subframe_count);
-        s.trav_count = uint32_t(std::min<size_t>(trav.bytes / sizeof(TravRec), 8 * (first_frame_node + frame_node_count)));
+        s.block_count = uint32_t(block_count);
+        s.spill = nullptr;
+        s.spill_stride = stack_bound;
         s.tri_count = uint32_t(index_count / 3);
         s.inst_count = uint32_t(instance_count);
         s.debug = PTG_DEBUG ? debug.as<uint32_t>() : nullptr;
@@ -934,6 +887,9 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     if(pm.npix == 0) return PTG_OK;
     if(j1 <= j0) return fail(PTG_E_INVALID, "empty sample range");
     const bool wf = ctx->pipeline == 0;
+    if(!wf && ctx->stack_bound >= PrivStack::kCap)
+        return fail(PTG_E_RANGE, "the megakernel's walk stack holds " + std::to_string(PrivStack::kCap) +
+                                     " entries, this frame's BVHs need " + std::to_string(ctx->stack_bound));
     // samples per chunk: megakernel <= 1 GiB of results; wavefront ~16 M live paths
     // Wavefront chunks are as large as HBM allows (capped at 35% of it): every
     // bounce round then launches over a long queue, so the walk and shade
@@ -1034,6 +990,15 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipStreamWaitEvent(ctx->acc_stream, ctx->ev_render_start, 0));
     }
     const DevScene sc = ctx->scene_args(cfg);
+    // walk stack spill areas: one per (chunk pipeline, walk kind), since up to
+    // four walk launches run at once; stack_bound entries per walk lane
+    const size_t spill_region = size_t(std::max(ctx->walk_grid[0], ctx->walk_grid[1])) * kBlock * ctx->stack_bound;
+    if(wf) PTG_HIP(ctx->spill.reserve(std::max<size_t>(1, 2 * nslots * spill_region) * sizeof(uint2)));
+    auto walk_scene = [&](uint32_t slot, int kind) {
+        DevScene w = sc;
+        w.spill = ctx->spill.as<uint2>() + (2 * slot + uint32_t(kind)) * spill_region;
+        return w;
+    };
     const uint32_t persistent = ctx->persistent_blocks;
     const bool overlap = wf && ctx->side != nullptr && ctx->concurrency >= 1;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
@@ -1043,6 +1008,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         const uint32_t nj = std::min(chunk, j1 - j);
         ptg_context::Slot& sl = slots[chunk_index % nslots];
         SlotState& sst = st[chunk_index % nslots];
+        const DevScene sc_ext = walk_scene(chunk_index % nslots, 0), sc_sh = walk_scene(chunk_index % nslots, 1);
         PathSoA* S = sst.S;
         TraceOut* trs = sst.trs;
         uint32_t** lists = sst.lists;
@@ -1086,10 +1052,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 const TraceOut& tr = trs[r & 1];
                 if(int e = timed_begin(ctx, K_EXTEND, ms)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
                 else
-                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
@@ -1100,10 +1066,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 {
                     if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
                     if(ctx->counting)
-                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc_sh,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
                     else
-                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc,
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc_sh,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
                     PTG_HIP(hipGetLastError());
                     if(int e = timed_end(ctx, ss)) return e;
@@ -1242,32 +1208,6 @@ int timed_end(ptg_context* ctx, hipStream_t st)
     return PTG_OK;
 }
 
-int pack_bvhs(ptg_context* ctx, const std::vector<BvhJob>& jobs, const ptg_bvh_node* nodes, const ptg_bvh_link* links,
-              TravRec* out)
-{
-    if(jobs.empty()) return PTG_OK;
-    PTG_HIP(ctx->jobs.reserve(jobs.size() * sizeof(BvhJob)));
-    PTG_HIP(hipMemcpyAsync(ctx->jobs.p, jobs.data(), jobs.size() * sizeof(BvhJob), hipMemcpyHostToDevice, ctx->stream));
-    uint32_t maxc = 0;
-    size_t link_end = 0;
-    for(const BvhJob& j: jobs)
-    {
-        maxc = std::max(maxc, 8 * j.count);
-        link_end = std::max(link_end, size_t(j.link_begin) + size_t(8) * j.count);
-    }
-    PTG_HIP(ctx->perm.reserve(link_end * sizeof(uint32_t)));
-    PTG_HIP(hipMemsetAsync(ctx->perm.p, 0xFF, link_end * sizeof(uint32_t), ctx->stream));
-    hipLaunchKernelGGL(k_preorder, dim3(grid_for(8 * jobs.size(), 64)), dim3(64), 0, ctx->stream, links,
-                       ctx->perm.as<uint32_t>(), ctx->jobs.as<BvhJob>(), uint32_t(jobs.size()));
-    PTG_HIP(hipGetLastError());
-    dim3 grid(std::min<uint32_t>(grid_for(maxc), 4096), uint32_t(jobs.size()));
-    hipLaunchKernelGGL(k_pack_bvh, grid, dim3(kBlock), 0, ctx->stream, nodes, links, ctx->perm.as<uint32_t>(), out,
-                       ctx->jobs.as<BvhJob>());
-    PTG_HIP(hipGetLastError());
-    PTG_HIP(hipStreamSynchronize(ctx->stream));   // jobs buffer is reused
-    return PTG_OK;
-}
-
 } // namespace
 
 extern "C" {
@@ -1297,19 +1237,16 @@ int ptg_context_create(int device, ptg_context** out)
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * per_cu_blocks;
     // walk grids: a multiple of what is resident at once (the queue is split
     // statically over the waves of the whole grid)
-#if PTG_WALK_LDS
-    // Walk residency: the walks' VGPRs (60-64) allow 8 blocks/CU, but at 8
-    // the sky and shade kernels on the other streams cannot get a wave onto a
-    // SIMD until walk waves retire.  The walk blocks' LDS (cold state padded)
-    // sets how many are resident: 7 (default) leaves 64 VGPRs per SIMD, one
-    // sky wave (PTG_SKY_WAVES 8 = 64 VGPRs).
-    uint32_t resident[2] = {7, 7};
+    // Walk residency: each walk lane holds its world ray (32 B) and its stack
+    // ring (8 x kRing B) in LDS, so the walk blocks' LDS sets how many are
+    // resident per CU (the LDS may be padded to hold fewer).
+    uint32_t resident[2] = {PTG_WALK_RESIDENT, PTG_WALK_RESIDENT};
     if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
+    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kRing);
     for(int k = 0; k < 2; ++k)
-        ctx->walk_lds[k] = std::max<uint32_t>(kBlock * sizeof(WalkCold), (lds_cu / resident[k]) / 1024u * 1024u);
-#endif
+        ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / resident[k]) / 1024u * 1024u);
     int per_cu = 0;
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, ctx->walk_lds[0]) == hipSuccess &&
        per_cu > 0)
@@ -1391,19 +1328,26 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     if(node_count >= (1u << 28) / 8 || index_count >= (1u << 31) || vertex_count >= (1u << 31))
         return fail(PTG_E_RANGE, "ptg_upload_scene: scene too large for 32-bit indexing");
     ctx->scene_ready = ctx->frame_ready = false;
-    ctx->packed_bvh.clear();
     ctx->packed_mesh.clear();
-    PTG_HIP(ctx->nodes.reserve(node_count * sizeof(ptg_bvh_node)));
-    PTG_HIP(ctx->links.reserve(8 * node_count * sizeof(ptg_bvh_link)));
+    ctx->cache.clear();
+    ctx->blas_on_device = 0;
+    try
+    {   // the BLASes are packed into blocks on the host when an instance first names them
+        ctx->host_nodes.assign(nodes, nodes + node_count);
+        ctx->host_links.assign(links, links + 8 * node_count);
+    }
+    catch(const std::bad_alloc&)
+    {
+        return fail(PTG_E_NOMEM, "ptg_upload_scene: host copy of the BVH nodes");
+    }
     PTG_HIP(ctx->indices.reserve(index_count * 4));
     PTG_HIP(ctx->pos.reserve(vertex_count * 16));
     PTG_HIP(ctx->normal.reserve(vertex_count * 16));
     PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
     PTG_HIP(ctx->material.reserve(vertex_count * 16));
-    PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec)));
+    // one 16 B record of slack: the walk reads a triangle as four 16-byte rows
+    PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 64));
     hipStream_t s = ctx->stream;
-    PTG_HIP(hipMemcpyAsync(ctx->nodes.p, nodes, node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
-    PTG_HIP(hipMemcpyAsync(ctx->links.p, links, 8 * node_count * sizeof(ptg_bvh_link), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->indices.p, indices, index_count * 4, hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->pos.p, pos, vertex_count * 16, hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->normal.p, normal, vertex_count * 16, hipMemcpyHostToDevice, s));
@@ -1417,52 +1361,35 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     return PTG_OK;
 }
 
-int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subframe_count,
-                     const ptg_tlas_instance* instances, size_t instance_count, const ptg_bvh_node* frame_nodes,
-                     const ptg_bvh_link* frame_links, size_t first_node, size_t frame_node_count)
+namespace {
+
+// The body of ptg_upload_frame (which adds the C ABI's exception barrier).
+int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subframe_count, const ptg_tlas_instance* instances,
+                 size_t instance_count, const ptg_bvh_node* frame_nodes, const ptg_bvh_link* frame_links, size_t first_node,
+                 size_t frame_node_count)
 {
-    if(int r = bind(ctx)) return r;
-    if(!ctx->scene_ready) return fail(PTG_E_INVALID, "ptg_upload_frame: upload the scene first");
-    if(!subframes || !subframe_count || !instances || !instance_count || !frame_nodes || !frame_links || !frame_node_count)
-        return fail(PTG_E_INVALID, "ptg_upload_frame: bad arguments");
-    if(first_node != ctx->static_nodes)
-        return fail(PTG_E_INVALID, "ptg_upload_frame: first_node must equal the uploaded static node count");
-    if((first_node + frame_node_count) * 8 >= (1ull << 32)) return fail(PTG_E_RANGE, "ptg_upload_frame: too many nodes");
     ctx->frame_ready = false;
     hipStream_t s = ctx->stream;
-    // one record buffer for both levels, indexed by global link index (BLAS:
-    // static nodes, TLAS: this frame's nodes after them), so a walk step
-    // addresses either level through the same pointer; growing it drops the
-    // packed BLAS records, which are then repacked below
-    {
-        const size_t need = 8 * (first_node + frame_node_count) * sizeof(TravRec);
-        if(need > ctx->trav.bytes)
-        {
-            PTG_HIP(hipStreamSynchronize(s));
-            PTG_HIP(ctx->trav.reserve(need + need / 8));
-            ctx->packed_bvh.clear();
-        }
-    }
 
-    // validate handles, pack instances, collect BLAS / mesh packing jobs.  The
-    // BLASes and meshes this call packs are collected locally and join the
-    // context's packed sets only after every check and every packing launch
-    // succeeded: an upload that fails half-way never leaves the sets claiming
-    // records that were not written.
+    // Validate every handle and pack the BLASes no earlier frame named plus
+    // this frame's TLASes (host/block_bvh.cpp, checked there before any
+    // kernel can follow a block link).  What this call packs joins the cache
+    // only after every upload succeeded: an upload that fails half-way never
+    // leaves the cache claiming records that were not written.
+    FramePack fp;
+    std::string err;
+    if(int r = ctx->cache.pack_frame(ctx->host_nodes.data(), ctx->host_links.data(), ctx->static_nodes, ctx->index_count,
+                                     ctx->vertex_count, subframes, subframe_count, instances, instance_count, frame_nodes,
+                                     frame_links, first_node, frame_node_count, fp, err))
+        return fail(r, "ptg_upload_frame: " + err);
     std::vector<InstTrav> it(instance_count);
     std::vector<InstShade> is(instance_count);
-    std::vector<BvhJob> blas_jobs;
     std::vector<MeshJob> mesh_jobs;
-    std::unordered_set<uint32_t> new_bvh, new_mesh;
+    std::unordered_set<uint32_t> new_mesh;
     for(size_t i = 0; i < instance_count; ++i)
     {
         const ptg_tlas_instance& in = instances[i];
-        if(uint64_t(in.blas.node_offset) + in.blas.node_count > ctx->static_nodes || in.blas.node_count == 0)
-            return fail(PTG_E_RANGE, "instance " + std::to_string(i) + ": BLAS outside the static nodes");
-        if(uint64_t(in.m.index_offset) + 3ull * in.m.triangle_count > ctx->index_count || in.m.index_offset % 3 ||
-           uint64_t(in.m.base_vertex_offset) + in.m.vertex_count > ctx->vertex_count)
-            return fail(PTG_E_RANGE, "instance " + std::to_string(i) + ": mesh outside the uploaded buffers");
-        const uint32_t handle[4] = {in.blas.node_count, in.blas.node_offset, in.m.index_offset / 3, 0u};
+        const uint32_t handle[4] = {fp.inst_root[i], in.m.index_offset / 3, 0u, 0u};
         for(int k = 0; k < 4; ++k)
         {
             float w;
@@ -1478,35 +1405,34 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
         is[i].index_offset = in.m.index_offset;
         is[i].base_vertex_offset = in.m.base_vertex_offset;
         std::fill(is[i].pad, is[i].pad + 5, 0u);
-        if(!ctx->packed_bvh.count(in.blas.node_offset) && new_bvh.insert(in.blas.node_offset).second)
-            blas_jobs.push_back(BvhJob{in.blas.node_offset, in.blas.node_offset * 8, in.blas.node_count,
-                                       in.blas.node_offset * 8});
         if(!ctx->packed_mesh.count(in.m.index_offset) && new_mesh.insert(in.m.index_offset).second)
             mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
     }
-    std::vector<BvhJob> tlas_jobs;
-    for(size_t i = 0; i < subframe_count; ++i)
-    {
-        const ptg_bvh& t = subframes[i].tlas;
-        if(t.node_offset < first_node || uint64_t(t.node_offset) + t.node_count > first_node + frame_node_count ||
-           t.node_count == 0)
-            return fail(PTG_E_RANGE, "subframe " + std::to_string(i) + ": TLAS outside the frame nodes");
-        const uint32_t rel = uint32_t(t.node_offset - first_node);
-        tlas_jobs.push_back(BvhJob{rel, rel * 8, t.node_count, uint32_t(t.node_offset) * 8});   // global link index
-        // every TLAS leaf must name a valid instance
-    }
-    for(size_t k = 0; k < 8 * frame_node_count; ++k)
-    {
-        const uint32_t a = frame_links[k].accept;
-        if((a & 0x80000000u) && (a & 0x7FFFFFFFu) >= instance_count)
-            return fail(PTG_E_RANGE, "TLAS leaf names instance " + std::to_string(a & 0x7FFFFFFFu));
-    }
 
+    // device copies: blocks = [BLAS blocks][TLAS blocks]; growing the buffer
+    // drops the BLAS blocks already there, which are then uploaded again
+    const std::vector<BlockEntry>& old_blas = ctx->cache.blas;
+    const size_t blas_total = old_blas.size() + fp.new_blas.size();
+    const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockEntry);
+    if(need > ctx->blocks.bytes)
+    {
+        PTG_HIP(hipStreamSynchronize(s));
+        ctx->blas_on_device = 0;
+        PTG_HIP(ctx->blocks.reserve(need + need / 8));
+    }
+    BlockEntry* dev = ctx->blocks.as<BlockEntry>();
+    if(ctx->blas_on_device < old_blas.size())
+        PTG_HIP(hipMemcpyAsync(dev + ctx->blas_on_device, old_blas.data() + ctx->blas_on_device,
+                               (old_blas.size() - ctx->blas_on_device) * sizeof(BlockEntry), hipMemcpyHostToDevice, s));
+    if(!fp.new_blas.empty())
+        PTG_HIP(hipMemcpyAsync(dev + old_blas.size(), fp.new_blas.data(), fp.new_blas.size() * sizeof(BlockEntry),
+                               hipMemcpyHostToDevice, s));
+    PTG_HIP(hipMemcpyAsync(dev + blas_total, fp.tlas.data(), fp.tlas.size() * sizeof(BlockEntry), hipMemcpyHostToDevice, s));
+    PTG_HIP(ctx->tlas_root.reserve(subframe_count * sizeof(uint32_t)));
+    PTG_HIP(hipMemcpyAsync(ctx->tlas_root.p, fp.tlas_root.data(), subframe_count * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     PTG_HIP(ctx->inst_trav.reserve(instance_count * sizeof(InstTrav)));
     PTG_HIP(ctx->inst_shade.reserve(instance_count * sizeof(InstShade)));
     PTG_HIP(ctx->subframes.reserve(subframe_count * sizeof(ptg_subframe)));
-    PTG_HIP(ctx->frame_nodes.reserve(frame_node_count * sizeof(ptg_bvh_node)));
-    PTG_HIP(ctx->frame_links.reserve(8 * frame_node_count * sizeof(ptg_bvh_link)));
     PTG_HIP(hipMemcpyAsync(ctx->inst_trav.p, it.data(), instance_count * sizeof(InstTrav), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->inst_shade.p, is.data(), instance_count * sizeof(InstShade), hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->subframes.p, subframes, subframe_count * sizeof(ptg_subframe), hipMemcpyHostToDevice, s));
@@ -1514,15 +1440,6 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
     hipLaunchKernelGGL(k_polygon_table, dim3(grid_for(subframe_count * kPolyStride)), dim3(kBlock), 0, s,
                        ctx->subframes.as<uint8_t>(), uint32_t(subframe_count), ctx->polygon.as<float2>());
     PTG_HIP(hipGetLastError());
-    PTG_HIP(hipMemcpyAsync(ctx->frame_nodes.p, frame_nodes, frame_node_count * sizeof(ptg_bvh_node), hipMemcpyHostToDevice, s));
-    PTG_HIP(hipMemcpyAsync(ctx->frame_links.p, frame_links, 8 * frame_node_count * sizeof(ptg_bvh_link),
-                           hipMemcpyHostToDevice, s));
-    if(int r = pack_bvhs(ctx, blas_jobs, ctx->nodes.as<ptg_bvh_node>(), ctx->links.as<ptg_bvh_link>(),
-                         ctx->trav.as<TravRec>()))
-        return r;
-    if(int r = pack_bvhs(ctx, tlas_jobs, ctx->frame_nodes.as<ptg_bvh_node>(), ctx->frame_links.as<ptg_bvh_link>(),
-                         ctx->trav.as<TravRec>()))
-        return r;
     if(!mesh_jobs.empty())
     {
         PTG_HIP(ctx->jobs.reserve(mesh_jobs.size() * sizeof(MeshJob)));
@@ -1534,16 +1451,45 @@ int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t sub
                            ctx->tris.as<TriRec>(), ctx->jobs.as<MeshJob>());
         PTG_HIP(hipGetLastError());
     }
-    PTG_HIP(hipStreamSynchronize(s));
-    ctx->packed_bvh.insert(new_bvh.begin(), new_bvh.end());
+    PTG_HIP(hipStreamSynchronize(s));   // the host vectors above are released on return
+
+    // commit
+    ctx->cache.commit(fp);
+    ctx->blas_on_device = ctx->cache.blas.size();
     ctx->packed_mesh.insert(new_mesh.begin(), new_mesh.end());
-    ctx->first_frame_node = first_node;
-    ctx->frame_node_count = frame_node_count;
+    ctx->block_count = fp.total_blocks();
+    ctx->stack_bound = fp.stack_bound();
+    ctx->host_tlas_root = fp.tlas_root;
     ctx->subframe_count = subframe_count;
     ctx->instance_count = instance_count;
     ctx->host_subframes.assign(subframes, subframes + subframe_count);
     ctx->frame_ready = true;
     return PTG_OK;
+}
+
+} // namespace
+
+int ptg_upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subframe_count,
+                     const ptg_tlas_instance* instances, size_t instance_count, const ptg_bvh_node* frame_nodes,
+                     const ptg_bvh_link* frame_links, size_t first_node, size_t frame_node_count)
+{
+    if(int r = bind(ctx)) return r;
+    if(!ctx->scene_ready) return fail(PTG_E_INVALID, "ptg_upload_frame: upload the scene first");
+    if(!subframes || !subframe_count || !instances || !instance_count || !frame_nodes || !frame_links || !frame_node_count)
+        return fail(PTG_E_INVALID, "ptg_upload_frame: bad arguments");
+    if(first_node != ctx->static_nodes)
+        return fail(PTG_E_INVALID, "ptg_upload_frame: first_node must equal the uploaded static node count");
+    if(first_node + frame_node_count >= (1ull << 31)) return fail(PTG_E_RANGE, "ptg_upload_frame: too many nodes");
+    try
+    {
+        return upload_frame(ctx, subframes, subframe_count, instances, instance_count, frame_nodes, frame_links, first_node,
+                            frame_node_count);
+    }
+    catch(const std::bad_alloc&)
+    {
+        ctx->frame_ready = false;
+        return fail(PTG_E_NOMEM, "ptg_upload_frame: host memory");
+    }
 }
 
 int ptg_upload_from_scene(ptg_context* ctx, const ptg_scene* scene, int include_static)
@@ -1628,6 +1574,7 @@ int ptg_path_trace_samples(ptg_context* ctx, const ptg_render_config* cfg, size_
     }
     if(uint64_t(jmax) / cfg->samples_per_motion_blur_step >= ctx->subframe_count)
         return fail(PTG_E_RANGE, "sample index beyond the frame's subframes");
+    if(ctx->stack_bound >= PrivStack::kCap) return fail(PTG_E_RANGE, "walk stack bound above the per-sample kernel's stack");
     PTG_HIP(ctx->tmp_a.reserve(n * sizeof(uint2)));
     PTG_HIP(ctx->tmp_b.reserve(n * sizeof(int32_t)));
     PTG_HIP(ctx->tmp_c.reserve(n * sizeof(float4)));
@@ -1667,9 +1614,9 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
     PTG_HIP(ctx->tmp_a.reserve(n * 32));
     PTG_HIP(ctx->tmp_b.reserve(n * 32));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, rays, n * 32, hipMemcpyHostToDevice, ctx->stream));
-    const ptg_bvh t = ctx->host_subframes[subframe].tlas;
-    hipLaunchKernelGGL(k_rays, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(nullptr), t.node_count,
-                       t.node_offset, uint32_t(n), ctx->tmp_a.as<float>(), ctx->tmp_b.as<uint32_t>());
+    if(ctx->stack_bound >= PrivStack::kCap) return fail(PTG_E_RANGE, "walk stack bound above the per-ray kernels' stack");
+    hipLaunchKernelGGL(k_rays, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(nullptr),
+                       ctx->host_tlas_root[subframe], uint32_t(n), ctx->tmp_a.as<float>(), ctx->tmp_b.as<uint32_t>());
     PTG_HIP(hipGetLastError());
     PTG_HIP(hipMemcpyAsync(hits, ctx->tmp_b.p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
     PTG_HIP(hipStreamSynchronize(ctx->stream));

@@ -1,0 +1,39 @@
+"""Block BVH records (csrc/device/block_format.h) on the CPU.
+
+tools/walk_sim runs the host half of ptg_upload_frame (BlockCache::pack_frame,
+host/block_bvh.cpp) on the real scene - a first frame committed, then the
+frame under test, so BLAS blocks are also packed at a nonzero block base -
+and walks a path-tracing query mix (camera rays, random bounces, sun shadow
+rays) twice: with the reference's stackless link walk (ray_query.hh:184-278)
+and with the device's block-walk algorithm over those blocks.  Every query
+must return the same hit bits (thit, barycentrics, instance, primitive,
+back face / occlusion).  The GPU kernels run the same algorithm and are
+checked bit for bit against the oracle by the -m gpu tests.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+TOOL = os.path.join(ROOT, "tools", "_bin", "walk_sim")
+
+
+@pytest.fixture(scope="module")
+def walk_sim(native_lib):
+    subprocess.run(["make", "-s", "walk_sim"], cwd=os.path.join(ROOT, "tools"), check=True)
+    return TOOL
+
+
+@pytest.mark.parametrize("frame", [0, 450, 1400])
+def test_block_walk_matches_link_walk(walk_sim, assets_dir, frame):
+    r = subprocess.run([walk_sim, assets_dir, str(frame), "3000", "16"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
+    assert m and int(m.group(1)) > 5000 and int(m.group(2)) == 0, r.stdout
+    # the block walk takes about half the dependent steps of the link walk
+    steps = [float(x) for x in re.findall(r"steps ([0-9.]+)", r.stdout)]
+    link_closest, block_closest = steps[0], steps[1]
+    assert block_closest < 0.6 * link_closest, r.stdout

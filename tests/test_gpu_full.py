@@ -189,7 +189,7 @@ def test_failed_frame_upload_leaves_no_stale_records(gpu, assets_dir):
     gpu.upload_arrays(arr, include_static=True, include_frame=False)
     bad = dict(arr)
     bad["instances"] = arr["instances"][: len(arr["instances"]) // 2]
-    with pytest.raises(N.PtgError, match=r"\(-6\).*TLAS leaf"):
+    with pytest.raises(N.PtgError, match=r"\(-6\).*TLAS.*leaf payload"):
         gpu.upload_arrays(bad, include_static=False)
     gpu.upload_arrays(arr, include_static=False)
     rect = (150, 80, 6, 4)
