@@ -58,6 +58,7 @@
 namespace ptg {
 
 constexpr uint32_t kBlockWidth = 4;
+constexpr uint32_t kBlockEntries = 8 * kBlockWidth;   // a block: one copy per octant
 
 struct alignas(16) BlockEntry {
     float lo_x, lo_y, lo_z;

@@ -65,6 +65,9 @@ struct Hit {
     bool back_face;
 };
 
+#ifndef PTG_PEND
+#define PTG_PEND 1   // park a reached triangle and keep walking (BlockWalker::park)
+#endif
 #ifndef PTG_PK_SLAB
 #define PTG_PK_SLAB 0
 #endif
@@ -77,6 +80,7 @@ PTG_D float wrcp(float x) { return rcp_rn(x); }
 PTG_D float wrcp(float x) { return 1.0f / x; }
 #endif
 PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : wrcp(d); }   // 1/d, 0 -> (float)1e40
+PTG_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 PTG_D uint32_t octant(f3 d) { return (d.x > 0 ? 1u : 0u) | (d.y > 0 ? 2u : 0u) | (d.z > 0 ? 4u : 0u); }
 
 // ray_triangle_intersection (math.hh:358-401) followed by the distance test of
@@ -232,64 +236,69 @@ struct PrivStack {
     PTG_D void reset() { sp = 0; }
     PTG_D uint32_t size() const { return sp; }
     PTG_D void reserve(uint32_t) {}
-    PTG_D void put(uint32_t k, uint2 e) { v[sp + k] = e; }   // entry sp + k, not yet pushed
-    PTG_D void advance(uint32_t k) { sp += k; }
+    PTG_D void put(uint2 e, bool keep) { v[sp] = e; sp += keep ? 1u : 0u; }
     PTG_D uint2 pop() { return v[--sp]; }
 };
 
-// LdsStack: the wavefront walks' stack.  The newest kRing entries of a lane
-// live in LDS (a ring, one 8-byte column per lane: slot k of a wave's 64
-// lanes is one conflict-free 512 B row); older ones spill to the lane's area
-// in HBM and come back when the stack unwinds to them.  A 12-entry ring holds
-// the whole stack for all but ~0.3 entries per query of a heavy frame.
+// LdsStack: the wavefront walks' stack.  The newest entries of a lane live
+// in LDS, in a window of kCap slots (one 8-byte column per lane: slot k of a
+// wave's 64 lanes is one conflict-free 512 B row), addressed through a
+// pointer to the next free slot, so a push is one ds_write at that pointer
+// and a pointer bump.  When a block step could overflow the window, its
+// oldest half goes to the lane's area in HBM and the rest moves down (rare);
+// those entries come back one by one when the stack unwinds to them.  A
+// 16-entry window holds the whole stack for all but ~0.03 entries per query
+// of a heavy frame.
 #ifndef PTG_LDS_STACK
-#define PTG_LDS_STACK 12
+#define PTG_LDS_STACK 16
 #endif
 struct LdsStack {
-    static constexpr uint32_t kRing = PTG_LDS_STACK;
-    lds_uint2_t* s;            // the lane's ring column: slot k at s[64 * k]
+    static constexpr uint32_t kCap = PTG_LDS_STACK;
+    lds_uint2_t* s;            // the lane's window column: slot k at s[64 * k]
+    lds_uint2_t* t;            // next free slot: s + 64 * (sp - lo)
     uint2* g;                  // the lane's spill area (HBM)
-    uint32_t sp, lo, top;      // entries; lowest entry still in the ring; ring slot of entry sp
-    PTG_D void reset() { sp = lo = top = 0; }
+    uint32_t sp, lo;           // entries; entries below lo are in HBM
+    PTG_D void reset()
+    {
+        sp = lo = 0;
+        t = s;
+    }
     PTG_D uint32_t size() const { return sp; }
-    // room for n more entries in the ring: the oldest go to HBM (rare)
+    // room for n more entries in the window (rare: spill the oldest half)
     PTG_D void reserve(uint32_t n)
     {
-        while(sp - lo + n > kRing)
+        if(sp - lo + n <= kCap) return;
+        const uint32_t in = sp - lo, h = in > 1 ? in / 2 : in;
+        for(uint32_t i = 0; i < h; ++i)
         {
-            uint32_t slot = top + kRing - (sp - lo);
-            if(slot >= kRing) slot -= kRing;
-            const lds_u2v v = s[64u * slot];
-            g[lo] = make_uint2(v.x, v.y);
-            ++lo;
+            const lds_u2v v = s[64u * i];
+            g[lo + i] = make_uint2(v.x, v.y);
         }
+        for(uint32_t i = h; i < in; ++i) s[64u * (i - h)] = s[64u * i];
+        lo += h;
+        t = s + 64u * (sp - lo);
     }
-    // entry sp + k (k < the room reserve() made), not yet pushed
-    PTG_D void put(uint32_t k, uint2 e)
+    // write e at the top; keep it (push) iff `keep`
+    PTG_D void put(uint2 e, bool keep)
     {
-        uint32_t slot = top + k;
-        if(slot >= kRing) slot -= kRing;
-        s[64u * slot] = lds_u2v{e.x, e.y};
-    }
-    PTG_D void advance(uint32_t k)
-    {
-        top += k;
-        if(top >= kRing) top -= kRing;
-        sp += k;
+        *t = lds_u2v{e.x, e.y};
+        if(keep)
+        {
+            t += 64;
+            ++sp;
+        }
     }
     PTG_D uint2 pop()
     {
         --sp;
-        top = top ? top - 1u : kRing - 1u;
-        const lds_u2v v = s[64u * top];
-        uint2 e = make_uint2(v.x, v.y);
         if(sp < lo)
-        {   // the ring was empty: the entry comes back from HBM (the ring
-            // slot read above held nothing; top is moot in an empty ring)
+        {   // the window is empty: the entry comes back from HBM
             lo = sp;
-            e = g[sp];
+            return g[sp];
         }
-        return e;
+        t -= 64;
+        const lds_u2v v = *t;
+        return make_uint2(v.x, v.y);
     }
 };
 
@@ -320,11 +329,15 @@ struct BlockWalker {
     float tmin, tmax;
     f3 org, inv;               // active level: ray origin / 1/dir in that level's space
     f3 winv;                   // the world ray's 1/dir (the TLAS level's inv)
+    bool fin;                  // active level: every component of inv finite (box_near_far applies)
     uint32_t oct;              // active level: direction octant (the links' order index, ray_query.hh:139-140)
     f3 S;                      // BLAS: shear constants of ray_triangle_intersection_preprocess
     int axis;                  // BLAS: dominant axis, -1 while in the TLAS (blas_axis)
     uint32_t tri_base, inst, bsp;
     uint32_t cur;              // next block, leaf word, or kBePop
+    float cnear;               // cur's entry distance (a leaf's is re-checked when it is tested)
+    uint32_t pend;             // PTG_PEND: a parked triangle (leaf word), or kBePop
+    float pnear;               // its entry distance
 
     // ray_query_initialize (ray_query.hh:111-151); root = the TLAS's root
     // block, kBePop for no TLAS (the walk ends at its first step)
@@ -337,6 +350,7 @@ struct BlockWalker {
         org = ro;
         inv = iw;
         winv = iw;
+        fin = finite3(iw);
         oct = octant(rd);
         S = V3(0, 0, 0);
         axis = -1;
@@ -345,6 +359,9 @@ struct BlockWalker {
         bsp = 0;
         st.reset();
         cur = root;
+        cnear = -__builtin_inff();
+        pend = kBePop;
+        pnear = 0.0f;
     }
     PTG_D Hit result() const { return cold.result(tmax); }
 
@@ -366,6 +383,22 @@ struct BlockWalker {
 #endif
         nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
         const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
+        return nearv <= farv && farv > tmin && nearv < tmax;
+    }
+
+    // The same test on a box stored as (near planes, far planes) for the
+    // ray's octant, for a level whose 1/dir is finite in every component:
+    // then t of the near plane IS fmin(t0, t1) of the reference's per-axis
+    // pair (the product of the ordered differences with a finite nonzero
+    // reciprocal keeps their order; equal values are equal), so the per-axis
+    // min/max drop out.  An unused slot's NaN planes fail it like any miss.
+    PTG_D bool box_near_far(float4 nr, float4 fr, float& nearv) const
+    {
+        const float tnx = (nr.x - org.x) * inv.x, tfx = (fr.x - org.x) * inv.x;
+        const float tny = (nr.y - org.y) * inv.y, tfy = (fr.y - org.y) * inv.y;
+        const float tnz = (nr.z - org.z) * inv.z, tfz = (fr.z - org.z) * inv.z;
+        nearv = fmaxf(tnx, fmaxf(tny, tnz));
+        const float farv = fminf(tfx, fminf(tfy, tfz));
         return nearv <= farv && farv > tmin && nearv < tmax;
     }
 
@@ -410,6 +443,7 @@ struct BlockWalker {
         const float k = 1.0f / rd.z;
 #endif
         S = V3(rd.x * k, rd.y * k, 1.0f * k);
+        fin = finite3(inv);
     }
 
     // ray_query_test_triangle + ray_triangle_intersection (ray_query.hh:225-246,
@@ -430,6 +464,27 @@ struct BlockWalker {
     }
 
     PTG_D bool at_leaf() const { return (cur & kBeLeaf) && cur != kBePop; }
+    // whether the leaf phase has work: a parked triangle, or a leaf in cur
+    PTG_D bool wants_leaf() const { return pend != kBePop || at_leaf(); }
+
+    // PTG_PEND: a triangle the walk reaches is parked (with its near) while
+    // the walk goes on with its next node steps; the leaf phase tests it.
+    // Triangles are still tested in the walk's order, each after a near <
+    // tmax re-check at its own time, and tmax changes only at triangle tests:
+    // the node steps taken meanwhile use a tmax that is, at worst, too large,
+    // which only adds work (block_format.h, facts 1 and 2).  BLAS entries are
+    // never parked, and a walk with a parked triangle does not leave its BLAS.
+    PTG_D void park()
+    {
+#if PTG_PEND
+        if(axis >= 0 && pend == kBePop && at_leaf())
+        {
+            pend = cur;
+            pnear = cnear;
+            cur = kBePop;
+        }
+#endif
+    }
 
     // Node phase: pop the next entry if the walk needs one, then, if it is a
     // block, one block step.  Returns 1 when the walk has ended, else 0 (the
@@ -444,82 +499,100 @@ struct BlockWalker {
                 if(st.size() == (axis < 0 ? 0u : bsp))
                 {
                     if(axis < 0) return 1;
+                    if(pend != kBePop) return 0;   // its parked triangle needs this BLAS: wait for the leaf phase
                     // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
                     axis = -1;
                     org = cold.world_o();
                     inv = winv;
+                    fin = finite3(winv);
                     oct = octant(cold.world_d());
                     continue;
                 }
                 const uint2 e = st.pop();
-                if(__uint_as_float(e.y) < tmax) { cur = e.x; break; }   // the entry's test at its own time
+                if(__uint_as_float(e.y) < tmax) { cur = e.x; cnear = __uint_as_float(e.y); break; }   // the entry's test at its own time
             }
-            if(cur & kBeLeaf) return 0;
+            if(cur & kBeLeaf)
+            {
+                park();
+                return 0;
+            }
         }
         const uint32_t w = cur;
         PTG_CHECK(sc, w < sc.block_count, kDebugNode);
-        // one block: four boxes, eight independent 16-byte loads
-        const v4f* p = reinterpret_cast<const v4f*>(sc.blocks + size_t(w) * kBlockWidth);
+        // this octant's copy of the block: its four entries in the order the
+        // ray meets them, each box as (near planes, far planes) for the
+        // octant's signs; eight independent 16-byte loads
+        const v4f* p = reinterpret_cast<const v4f*>(sc.blocks + (size_t(w) * 8u + oct) * kBlockWidth);
         const v4f q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4], q5 = p[5], q6 = p[6], q7 = p[7];
         const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q1.x, q1.y, q1.z, q1.w);
         const float4 l1 = make_float4(q2.x, q2.y, q2.z, q2.w), h1 = make_float4(q3.x, q3.y, q3.z, q3.w);
         const float4 l2 = make_float4(q4.x, q4.y, q4.z, q4.w), h2 = make_float4(q5.x, q5.y, q5.z, q5.w);
         const float4 l3 = make_float4(q6.x, q6.y, q6.z, q6.w), h3 = make_float4(q7.x, q7.y, q7.z, q7.w);
         if(COUNT) cnt.step_loads |= 1u;
-        uint32_t b0 = __float_as_uint(h0.w), b1 = __float_as_uint(h1.w), b2 = __float_as_uint(h2.w), b3 = __float_as_uint(h3.w);
-        // keep the order words in the registers the block load filled (the
-        // compiler would otherwise re-load the one the select picks)
-        asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
-        const uint32_t ob = oct >> 1;
-        const uint32_t pw = ob < 2u ? (ob ? b1 : b0) : (ob == 3u ? b3 : b2);
-        const uint32_t perm = (oct & 1u) ? pw >> 16 : pw;
         const uint32_t a0 = __float_as_uint(l0.w), a1 = __float_as_uint(l1.w), a2 = __float_as_uint(l2.w),
                        a3 = __float_as_uint(l3.w);
         float n0, n1, n2, n3;
-        const bool p0 = box(l0, h0, n0) && !(a0 & kBeNone), p1 = box(l1, h1, n1) && !(a1 & kBeNone);
-        const bool p2 = box(l2, h2, n2) && !(a2 & kBeNone), p3 = box(l3, h3, n3) && !(a3 & kBeNone);
+        bool p0, p1, p2, p3;
+        if(__all(fin))
+        {   // every lane's reciprocal finite (the rule): no per-axis min/max
+            p0 = box_near_far(l0, h0, n0); p1 = box_near_far(l1, h1, n1);
+            p2 = box_near_far(l2, h2, n2); p3 = box_near_far(l3, h3, n3);
+        }
+        else
+        {   // a lane with a zero or denormal direction component: the
+            // reference's min/max form (an unordered pair gives the same)
+            p0 = box(l0, h0, n0); p1 = box(l1, h1, n1); p2 = box(l2, h2, n2); p3 = box(l3, h3, n3);
+        }
         if(COUNT)
         {
             const uint32_t tested = !(a0 & kBeNone) + !(a1 & kBeNone) + !(a2 & kBeNone) + !(a3 & kBeNone);
             cnt.visits += tested;
             if(axis < 0) cnt.tlas_visits += tested;
         }
+        // bit j: the entry the ray meets j-th passed.  The first is walked
+        // next; the others are pushed last-first, so they pop in order.
         const uint32_t hits = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
-        // passing entries in the ray's order: bit j = the entry met j-th
-        const uint32_t om = ((hits >> (perm & 3u)) & 1u) | (((hits >> ((perm >> 4) & 3u)) & 1u) << 1) |
-                            (((hits >> ((perm >> 8) & 3u)) & 1u) << 2) | (((hits >> ((perm >> 12) & 3u)) & 1u) << 3);
-        // slot t's word / near: two selects on t's bits (no branches)
-        const uint32_t m0 = __float_as_uint(n0), m1 = __float_as_uint(n1), m2 = __float_as_uint(n2),
-                       m3 = __float_as_uint(n3);
-        auto slot_a = [=](uint32_t t) { return sel4(t, a0, a1, a2, a3); };
-        auto slot_n = [=](uint32_t t) { return sel4(t, m0, m1, m2, m3); };
-        // the first is walked next; the others are pushed last-first, so they
-        // pop in the ray's order
-        const uint32_t first = (perm >> (4u * uint32_t(__builtin_ctz(om | 16u)))) & 3u;
-        cur = om ? slot_a(first) : kBePop;
-        const uint32_t rest = om & (om - 1u);
+        const uint32_t first = uint32_t(__builtin_ctz(hits | 16u)) & 3u;
+        cur = hits ? sel4(first, a0, a1, a2, a3) : kBePop;
+        cnear = __uint_as_float(sel4(first, __float_as_uint(n0), __float_as_uint(n1), __float_as_uint(n2),
+                                     __float_as_uint(n3)));
+        const uint32_t rest = hits & (hits - 1u);
         if(rest)
-        {
+        {   // written at the top either way, kept only if pushed
             st.reserve(kBlockWidth - 1);
-            uint32_t k = 0;
-#pragma unroll
-            for(uint32_t j = kBlockWidth - 1; j >= 1; --j)
-            {   // written into the reserved room either way, kept only if pushed
-                const uint32_t t = (perm >> (4u * j)) & 3u;
-                st.put(k, make_uint2(slot_a(t), slot_n(t)));
-                k += (rest >> j) & 1u;
-            }
-            st.advance(k);
+            st.put(make_uint2(a3, __float_as_uint(n3)), (rest >> 3) & 1u);
+            st.put(make_uint2(a2, __float_as_uint(n2)), (rest >> 2) & 1u);
+            st.put(make_uint2(a1, __float_as_uint(n1)), (rest >> 1) & 1u);
         }
+        park();
         return 0;
     }
 
-    // Leaf phase: the triangle test, or the BLAS entry, the walk stands at.
-    // Returns 0, or 2 (ANY only) when the triangle occludes the ray.
+    // Leaf phase: the parked triangle, else the BLAS entry or triangle the
+    // walk stands at.  Returns 0, or 2 (ANY only) when a triangle occludes
+    // the ray.
     template<bool ANY, bool COUNT>
     PTG_D int leaf_step(const DevScene& sc, Counters& cnt)
     {
+#if PTG_PEND
+        if(pend != kBePop)
+        {
+            const uint32_t id = pend & kBeIndex;
+            const float n = pnear;
+            pend = kBePop;
+            if(n < tmax)   // the triangle's box test at its own time
+            {
+                if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
+                PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
+                const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + id);
+                if(const int r = tri_test<ANY>(id, tp[0], tp[1], tp[2])) return r;
+            }
+            park();   // a triangle waiting in cur is parked next
+            return 0;
+        }
+#endif
         const uint32_t id = cur & kBeIndex;
+        const float n = cnear;
         cur = kBePop;
         if(axis < 0)
         {
@@ -531,6 +604,7 @@ struct BlockWalker {
             enter(id, ip[0], ip[1], ip[2], ip[3]);
             return 0;
         }
+        if(!(n < tmax)) return 0;   // re-checked at its own time (a triangle reached behind a parked one)
         if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
         PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
         const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + id);
@@ -543,7 +617,7 @@ struct BlockWalker {
     template<bool ANY, bool COUNT>
     PTG_D int step(const DevScene& sc, Counters& cnt)
     {
-        if(at_leaf()) return leaf_step<ANY, COUNT>(sc, cnt);
+        if(wants_leaf()) return leaf_step<ANY, COUNT>(sc, cnt);
         return node_step<COUNT>(sc, cnt);
     }
 };

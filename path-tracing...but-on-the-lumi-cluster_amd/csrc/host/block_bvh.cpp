@@ -191,18 +191,19 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
         blks.push_back(make(0));
     for(size_t q = 0; q < blks.size(); ++q)            // breadth-first
     {
-        block_of[blks[q].root] = block_base + uint32_t(out.size() / W + q);
+        block_of[blks[q].root] = block_base + uint32_t(out.size() / kBlockEntries + q);
         for(uint32_t c: std::vector<uint32_t>(blks[q].slots))
             if(!t.leaf(c)) blks.push_back(make(c));
     }
-    if(uint64_t(block_base) + out.size() / W + blks.size() > kBeIndex) { err = "BVH records above 2^28 blocks"; return false; }
-    if(out.size() % W) { err = "unaligned block output"; return false; }
+    if(uint64_t(block_base) + out.size() / kBlockEntries + blks.size() > kBeIndex)
+    { err = "BVH records above 2^28 blocks"; return false; }
+    if(out.size() % kBlockEntries) { err = "unaligned block output"; return false; }
 
     // stack bound: a block step walks one passing entry and pushes the
     // others (at most all but one); a walk holds at most one block's pushes
     // per level of its path
     std::vector<uint32_t> bound(blks.size(), 0);
-    const uint32_t first = uint32_t(out.size() / W) + block_base;
+    const uint32_t first = uint32_t(out.size() / kBlockEntries) + block_base;
     for(size_t q = blks.size(); q-- > 0;)
     {
         uint32_t own = uint32_t(blks[q].slots.size()) - 1u, below = 0;
@@ -215,19 +216,10 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
 
     for(const Blk& b: blks)
     {
-        BlockEntry e[kBlockWidth];
-        for(uint32_t s = 0; s < W; ++s)
-        {
-            if(s >= b.slots.size()) { e[s] = none_entry(); continue; }
-            const uint32_t c = b.slots[s];
-            const ptg_bvh_node& n = t.box[c];
-            e[s].lo_x = n.min_x; e[s].lo_y = n.min_y; e[s].lo_z = n.min_z;
-            e[s].hi_x = n.max_x; e[s].hi_y = n.max_y; e[s].hi_z = n.max_z;
-            e[s].a = t.leaf(c) ? t.payload[c] : block_of[c];
-            e[s].b = 0;
-        }
-        // slot order per octant: depth-first through the expanded nodes, each
-        // one's children forward or reversed by its axis (bvh.cc:177-181)
+        // one copy per octant o: the entries in the order a ray of that
+        // octant meets them (depth-first through the expanded nodes, each
+        // one's children forward or reversed by its axis, bvh.cc:177-181),
+        // each box as (near planes, far planes) for that octant's signs
         for(uint32_t o = 0; o < 8; ++o)
         {
             std::vector<uint32_t> seq;
@@ -238,18 +230,29 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
                 {
                     const uint32_t c = ks[rev ? ks.size() - 1 - j : j];
                     if(std::find(b.expanded.begin(), b.expanded.end(), c) != b.expanded.end()) self(self, c);
-                    else seq.push_back(uint32_t(std::find(b.slots.begin(), b.slots.end(), c) - b.slots.begin()));
+                    else seq.push_back(c);
                 }
             };
-            if(t.leaf(b.root)) seq.push_back(0);
+            if(t.leaf(b.root)) seq.push_back(b.root);
             else walk(walk, b.root);
-            uint32_t p = 0;
-            for(uint32_t j = 0; j < W; ++j) p |= (j < seq.size() ? seq[j] : j) << (4 * j);
-            e[o >> 1].b |= p << (16 * (o & 1));
+            if(seq.size() != b.slots.size()) { err = "block order lost an entry"; return false; }
+            for(uint32_t j = 0; j < W; ++j)
+            {
+                if(j >= seq.size()) { out.push_back(none_entry()); continue; }
+                const uint32_t c = seq[j];
+                const ptg_bvh_node& n = t.box[c];
+                const bool px = o & 1u, py = o & 2u, pz = o & 4u;
+                BlockEntry e;
+                e.lo_x = px ? n.min_x : n.max_x; e.hi_x = px ? n.max_x : n.min_x;
+                e.lo_y = py ? n.min_y : n.max_y; e.hi_y = py ? n.max_y : n.min_y;
+                e.lo_z = pz ? n.min_z : n.max_z; e.hi_z = pz ? n.max_z : n.min_z;
+                e.a = t.leaf(c) ? t.payload[c] : block_of[c];
+                e.b = 0;
+                out.push_back(e);
+            }
         }
-        for(uint32_t s = 0; s < W; ++s) out.push_back(e[s]);
     }
-    info.root = block_base + uint32_t((out.size() / W) - blks.size());
+    info.root = block_base + uint32_t((out.size() / kBlockEntries) - blks.size());
     info.blocks = uint32_t(blks.size());
     info.stack_entries = bound.empty() ? 0 : bound[0];
     info.max_payload = 0;
@@ -268,9 +271,8 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
                            const ptg_bvh_link* frame_links, size_t first_node, size_t frame_node_count, FramePack& fp,
                            std::string& err) const
 {
-    const uint32_t W = kBlockWidth;
     fp = FramePack();
-    fp.blas_base = uint32_t(blas.size() / W);
+    fp.blas_base = uint32_t(blas.size() / kBlockEntries);
     fp.blas_stack = blas_stack;
     fp.inst_root.resize(instance_count);
     std::string why;
@@ -308,7 +310,7 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
         }
         fp.inst_root[i] = rec.root;
     }
-    fp.tlas_base = fp.blas_base + uint32_t(fp.new_blas.size() / W);
+    fp.tlas_base = fp.blas_base + uint32_t(fp.new_blas.size() / kBlockEntries);
     fp.tlas_root.resize(subframe_count);
     for(size_t i = 0; i < subframe_count; ++i)
     {

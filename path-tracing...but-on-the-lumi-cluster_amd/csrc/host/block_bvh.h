@@ -16,8 +16,8 @@ struct BlockBvh {
 
 // Packs one BVH given in the reference layout - nodes[0..count) and the eight
 // link orders links[o * count + i] (bvh.cc:195-229) - appending its blocks
-// (kBlockWidth entries each) to `out`.  Child block indices are block_base +
-// position in `out` / kBlockWidth.  Checked, with an error in `err`:
+// (kBlockEntries entries each: kBlockWidth per octant) to `out`.  Child block
+// indices are block_base + position in `out` / kBlockEntries.  Checked, with an error in `err`:
 //   - the links are the reference builder's: a tree rooted at node 0 whose
 //     every order lists each node's children forward, or reversed when the
 //     octant's sign on the node's axis is not positive (bvh.cc:173-191);
@@ -49,7 +49,7 @@ struct FramePack {
     std::vector<uint32_t> tlas_root;        // per subframe
     std::vector<uint32_t> inst_root;        // per instance: its BLAS's root block
     uint32_t blas_stack = 0, tlas_stack = 0;
-    uint32_t total_blocks() const { return tlas_base + uint32_t(tlas.size() / kBlockWidth); }
+    uint32_t total_blocks() const { return tlas_base + uint32_t(tlas.size() / kBlockEntries); }
     uint32_t stack_bound() const { return blas_stack + tlas_stack; }   // stack entries a walk can hold
 };
 

@@ -225,7 +225,7 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
 #endif
 #ifndef PTG_WALK_RESIDENT
-#define PTG_WALK_RESIDENT 5 // walk blocks per CU (LDS-bound with 12-entry stack rings: 5 x 32 KB)
+#define PTG_WALK_RESIDENT 4 // walk blocks per CU (LDS-bound with 16-entry stack windows: 4 x 40 KB)
 #endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
@@ -256,12 +256,12 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
-    // LDS: every lane's world ray, then the stack rings, one 64-lane x kRing
+    // LDS: every lane's world ray, then the stack windows, one 64-lane x kCap
     // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
     BlockWalker<LdsCold, LdsStack> w;
     w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C casts: generic -> LDS address space
-    w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kRing) + lane);
+    w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);
     w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
     bool active = false;
     uint32_t q = 0;
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
 #if PTG_VMEM_STATS
             if(COUNT) cnt.step_loads = 0;
 #endif
-            if(active && !w.at_leaf()) r = w.template node_step<COUNT>(sc, cnt);
+            if(active && !w.at_leaf()) r = w.template node_step<COUNT>(sc, cnt);   // (a lane with a parked triangle walks on)
 #if PTG_VMEM_STATS
             if(COUNT)
             {
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
 #if PTG_VMEM_STATS
         if(COUNT) cnt.step_loads = 0;
 #endif
-        if(active && w.at_leaf())
+        if(active && w.wants_leaf())
         {
             r = w.template leaf_step<ANY, COUNT>(sc, cnt);
             if(r != 0) { finish(r); active = false; }
@@ -1238,13 +1238,13 @@ int ptg_context_create(int device, ptg_context** out)
     // walk grids: a multiple of what is resident at once (the queue is split
     // statically over the waves of the whole grid)
     // Walk residency: each walk lane holds its world ray (32 B) and its stack
-    // ring (8 x kRing B) in LDS, so the walk blocks' LDS sets how many are
+    // window (8 x kCap B) in LDS, so the walk blocks' LDS sets how many are
     // resident per CU (the LDS may be padded to hold fewer).
     uint32_t resident[2] = {PTG_WALK_RESIDENT, PTG_WALK_RESIDENT};
     if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
-    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kRing);
+    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kCap);
     for(int k = 0; k < 2; ++k)
         ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / resident[k]) / 1024u * 1024u);
     int per_cu = 0;

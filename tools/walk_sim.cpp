@@ -42,7 +42,7 @@ struct Res {
 };
 struct Stats {
     double queries = 0, visits = 0, steps = 0, dep_loads = 0, bytes = 0, tri = 0, enters = 0;
-    double block_steps = 0, leaf_steps = 0, pushes = 0, pops = 0, spills = 0, culled = 0;
+    double block_steps = 0, leaf_steps = 0, pushes = 0, pops = 0, spills = 0, culled = 0, iters = 0;
     std::map<uint32_t, uint64_t> depth_hist;
 };
 
@@ -173,108 +173,175 @@ Res link_walk(const ptg_scene_view& v, const Query& q, Stats& st)
 constexpr uint32_t POP = 0xFFFFFFFFu;
 
 // ---- block walk (production packer, device algorithm) -----------------------
+bool g_spec = true;   // SPEC=0: no parked triangles
+
 struct Packed {
     std::vector<BlockEntry> E;         // the device block buffer: [BLAS blocks][TLAS blocks]
     std::vector<uint32_t> inst_root;   // per instance: BLAS root block
     std::vector<uint32_t> tlas_root;   // per subframe
 };
 
-Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats& st, uint32_t C)
-{
-    std::vector<std::pair<uint32_t, uint32_t>> stack;   // (near bits, word) entries, as the device's
-    uint32_t bsp = 0;
-    Res best;
-    float tmax = q.tmax;
-    f3 org = q.o, dir = q.d, inv = v3(srcp(q.d.x), srcp(q.d.y), srcp(q.d.z));
-    const f3 winv = inv;
+// The device walker (path_tracer.h BlockWalker) step for step: node steps
+// (pop + block) and leaf steps (parked triangle / BLAS entry / triangle),
+// scheduled as the wavefront walk kernel does (U node phases, one leaf phase).
+struct SimWalker {
+    const ptg_scene_view& v;
+    const Packed& pk;
+    const Query& q;
+    Stats& st;
+    uint32_t C;                                         // LDS ring entries (spill counting)
+    std::vector<std::pair<uint32_t, uint32_t>> stack;   // (word, near bits)
+    uint32_t bsp = 0, cur, pend = kBePop, maxd = 0;
+    float tmax, cnear = -INFINITY, pnear = 0;
+    f3 org, dir, inv, winv;
     int axis = -1;
     Blas b{};
-    uint32_t cur = pk.tlas_root[q.subframe];
-    uint32_t maxd = 0;
-    st.queries++;
-    auto push = [&](uint32_t nb, uint32_t w) {
-        stack.push_back({nb, w});
+    Res best;
+    bool spec;
+
+    SimWalker(const ptg_scene_view& v_, const Packed& pk_, const Query& q_, Stats& st_, uint32_t C_, bool spec_)
+        : v(v_), pk(pk_), q(q_), st(st_), C(C_), spec(spec_)
+    {
+        tmax = q.tmax;
+        org = q.o; dir = q.d;
+        inv = winv = v3(srcp(q.d.x), srcp(q.d.y), srcp(q.d.z));
+        cur = pk.tlas_root[q.subframe];
+    }
+    bool at_leaf() const { return (cur & kBeLeaf) && cur != kBePop; }
+    bool wants_leaf() const { return pend != kBePop || at_leaf(); }
+    void park()
+    {
+        if(spec && axis >= 0 && pend == kBePop && at_leaf()) { pend = cur; pnear = cnear; cur = kBePop; }
+    }
+    void push(uint32_t w, float n)
+    {
+        uint32_t nb;
+        memcpy(&nb, &n, 4);
+        stack.push_back({w, nb});
         st.pushes++;
         if(stack.size() > C) st.spills++;
         maxd = std::max<uint32_t>(maxd, uint32_t(stack.size()));
-    };
-    for(;;)
+    }
+    int node_step()
     {
         if(cur == kBePop)
         {
             for(;;)
             {
-                const uint32_t base = axis < 0 ? 0u : bsp;
-                if(stack.size() == base)
+                if(stack.size() == (axis < 0 ? 0u : bsp))
                 {
-                    if(axis < 0) break;
+                    if(axis < 0) return 1;
+                    if(pend != kBePop) return 0;
                     axis = -1; org = q.o; dir = q.d; inv = winv;
                     continue;
                 }
-                const uint32_t w = stack.back().second;
-                float n;
-                memcpy(&n, &stack.back().first, 4);
+                const auto e = stack.back();
                 stack.pop_back();
                 st.pops++;
-                if(n < tmax) { cur = w; break; }
+                float n;
+                memcpy(&n, &e.second, 4);
+                if(n < tmax) { cur = e.first; cnear = n; break; }
             }
-            if(cur == kBePop) break;
+            if(cur & kBeLeaf) { park(); return 0; }
         }
         st.steps++;
-        if(cur & kBeLeaf)
-        {
-            const uint32_t idx = cur & kBeIndex;
-            cur = kBePop;
-            st.leaf_steps++;
-            if(axis < 0)
-            {
-                st.enters++;
-                st.bytes += 64;
-                const ptg_tlas_instance& in = v.instances[idx];
-                b = enter(in, idx, q.o, q.d);
-                axis = b.axis; bsp = uint32_t(stack.size());
-                org = b.org; inv = b.inv; dir = b.bd;
-                cur = pk.inst_root[idx];
-                continue;
-            }
-            st.tri++;
-            st.bytes += 48;
-            Res c;
-            if(tri(b, v, idx, q.tmin, tmax, c))
-            {
-                if(q.any) { best.occluded = true; break; }
-                best = c;
-                tmax = c.t;
-            }
-            continue;
-        }
         st.block_steps++;
         st.bytes += 128;
-        const BlockEntry* e = &pk.E[size_t(cur) * kBlockWidth];
-        const uint32_t o = octant(dir);
-        const uint32_t perm = (e[o >> 1].b >> (16 * (o & 1))) & 0xFFFFu;
+        // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
+        const BlockEntry* e = &pk.E[(size_t(cur) * 8u + octant(dir)) * kBlockWidth];
+        const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
         for(int j = int(kBlockWidth) - 1; j >= 0; --j)
         {
-            const BlockEntry& x = e[(perm >> (4 * j)) & 15u];
+            const BlockEntry& x = e[j];
             if(x.a & kBeNone) continue;
             float n;
             st.visits++;
-            if(!box(org, inv, q.tmin, tmax, &x.lo_x, &x.hi_x, n)) continue;
-            if(cand != kBePop)
-            {
-                uint32_t nb;
-                memcpy(&nb, &cn, 4);
-                push(nb, cand);
+            bool pass;
+            if(fin)
+            {   // the device's fast form: near = max of near-plane t, far = min of far-plane t
+                const float tnx = (x.lo_x - org.x) * inv.x, tfx = (x.hi_x - org.x) * inv.x;
+                const float tny = (x.lo_y - org.y) * inv.y, tfy = (x.hi_y - org.y) * inv.y;
+                const float tnz = (x.lo_z - org.z) * inv.z, tfz = (x.hi_z - org.z) * inv.z;
+                n = fmaxf_(tnx, fmaxf_(tny, tnz));
+                const float f = fminf_(tfx, fminf_(tfy, tfz));
+                pass = n <= f && f > q.tmin && n < tmax;
             }
+            else
+                pass = box(org, inv, q.tmin, tmax, &x.lo_x, &x.hi_x, n);
+            if(!pass) continue;
+            if(cand != kBePop) push(cand, cn);
             cand = x.a;
             cn = n;
         }
         cur = cand;
+        cnear = cn;
+        park();
+        return 0;
     }
-    st.depth_hist[maxd]++;
-    return best;
+    int tri_at(uint32_t id, float n)
+    {
+        if(!(n < tmax)) return 0;
+        st.steps++;
+        st.leaf_steps++;
+        st.tri++;
+        st.bytes += 48;
+        Res c;
+        if(tri(b, v, id, q.tmin, tmax, c))
+        {
+            if(q.any) { best.occluded = true; return 2; }
+            best = c;
+            tmax = c.t;
+        }
+        return 0;
+    }
+    int leaf_step()
+    {
+        if(pend != kBePop)
+        {
+            const uint32_t id = pend & kBeIndex;
+            const float n = pnear;
+            pend = kBePop;
+            if(int r = tri_at(id, n)) return r;
+            park();
+            return 0;
+        }
+        const uint32_t id = cur & kBeIndex;
+        const float n = cnear;
+        cur = kBePop;
+        if(axis < 0)
+        {
+            st.steps++;
+            st.leaf_steps++;
+            st.enters++;
+            st.bytes += 64;
+            const ptg_tlas_instance& in = v.instances[id];
+            b = enter(in, id, q.o, q.d);
+            axis = b.axis; bsp = uint32_t(stack.size());
+            org = b.org; inv = b.inv; dir = b.bd;
+            cur = pk.inst_root[id];
+            return 0;
+        }
+        return tri_at(id, n);
+    }
+};
+
+Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats& st, uint32_t C)
+{
+    st.queries++;
+    SimWalker w(v, pk, q, st, C, g_spec);
+    for(;;)
+    {
+        int r = 0;
+        for(int u = 0; u < 2 && r == 0; ++u)
+            if(!w.at_leaf()) r = w.node_step();
+        if(r == 0 && w.wants_leaf()) r = w.leaf_step();
+        if(r) break;
+        st.iters++;
+    }
+    st.depth_hist[w.maxd]++;
+    return w.best;
 }
 
 uint64_t rng_state = 0x9E3779B97F4A7C15ull;
@@ -292,6 +359,7 @@ int main(int argc, char** argv)
     const uint32_t frame = uint32_t(atoi(argv[2]));
     const uint32_t paths = argc > 3 ? uint32_t(atoi(argv[3])) : 20000;
     const uint32_t S = argc > 4 ? uint32_t(atoi(argv[4])) : 16;
+    if(const char* e = getenv("SPEC")) g_spec = atoi(e) != 0;
     ptg_render_config cfg;
     ptg_render_config_default(&cfg);
     cfg.width = 1280; cfg.height = 720; cfg.samples_per_pixel = 1024;
@@ -384,9 +452,9 @@ int main(int argc, char** argv)
         printf("%s: %.0f queries\n", k ? "shadow (any)" : "closest", a.queries);
         printf("  link : visits %.1f  steps %.1f  dep-loads %.1f  tri %.2f  enters %.2f  bytes %.0f\n", a.visits / a.queries,
                a.steps / a.queries, a.dep_loads / a.queries, a.tri / a.queries, a.enters / a.queries, a.bytes / a.queries);
-        printf("  block: boxes %.1f  steps %.1f (block %.1f, leaf %.1f)  tri %.2f  enters %.2f  pushes %.1f  spills(S=%u) %.3f  culled-leaves %.2f  bytes %.0f\n",
+        printf("  block: boxes %.1f  steps %.1f (block %.1f, leaf %.1f)  tri %.2f  enters %.2f  pushes %.1f  spills(S=%u) %.3f  iters %.1f  bytes %.0f\n",
                b.visits / b.queries, b.steps / b.queries, b.block_steps / b.queries, b.leaf_steps / b.queries, b.tri / b.queries,
-               b.enters / b.queries, b.pushes / b.queries, S, b.spills / b.queries, b.culled / b.queries, b.bytes / b.queries);
+               b.enters / b.queries, b.pushes / b.queries, S, b.spills / b.queries, b.iters / b.queries, b.bytes / b.queries);
         uint64_t acc = 0;
         printf("  max stack depth CDF:");
         for(auto& kv: b.depth_hist)
