@@ -91,10 +91,12 @@ def algorithmic_bytes(c):
 
 
 def extend_bytes(c):
-    """Algorithmic bytes of the closest-hit walk kernel: per node visit 32 B
-    (node + link), per triangle test 60 B (3 x u32 + 3 x 16 B in reference
-    layout), per BLAS entry 88 B, plus per ray 48 B of ray state in and 32 B
-    of hit out."""
+    """Algorithmic bytes of the closest-hit walk kernel: per box test 32 B (the
+    reference's node + link per visit; one 32 B block entry of the block
+    walker, which tests about as many boxes as the reference visits nodes:
+    DESIGN.md section 4), per triangle test 60 B (3 x u32 + 3 x 16 B in
+    reference layout), per BLAS entry 88 B, plus per ray 48 B of ray state in
+    and 32 B of hit out."""
     visits, tris, enters, queries = int(c[1]), int(c[2]), int(c[3]), int(c[4])
     return 32 * visits + 60 * tris + 88 * enters + 80 * queries
 
@@ -112,6 +114,11 @@ def hierarchy_roofline(ent, launch_s, bytes_per_launch):
                   random-line rate
       hbm         HBM-side bytes (FETCH_SIZE x 2 + WRITE_SIZE, the guide's
                   gfx950 correction) vs 8 TB/s
+      valu_issue  wave-level VALU instructions (SQ_INSTS_VALU) x 2 cycles per
+                  SIMD (wave64 FP32 issue on gfx950, MI355X_MICROARCH.md) over
+                  the 1024 SIMDs at the clock the profile measured
+      salu_issue  wave-level SALU instructions (SQ_INSTS_SALU), one per cycle
+                  per CU (256)
 
     Each level's time is count / rate; the largest is the floor t_min and
     names the bound.  frac = t_min / measured time (<= 1 by construction when
@@ -134,6 +141,11 @@ def hierarchy_roofline(ent, launch_s, bytes_per_launch):
     level("l2", pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"], ceil["l2_lines_per_s"], "64-B line requests")
     level("fabric", pmc["TCC_MISS_sum"], ceil["ic_lines_per_s"], "64-B line requests (L2 misses)")
     level("hbm", d["hbm_side_bytes"], HBM_PEAK_GBS * 1e9, "bytes")
+    clock = d.get("clock_GHz") or 2.4
+    if "SQ_INSTS_VALU" in pmc:
+        level("valu_issue", pmc["SQ_INSTS_VALU"] * 2.0, 1024 * clock * 1e9, "SIMD cycles (2 per wave64 VALU)")
+    if "SQ_INSTS_SALU" in pmc:
+        level("salu_issue", pmc["SQ_INSTS_SALU"], 256 * clock * 1e9, "CU scalar cycles")
     bound = max(levels, key=lambda k: levels[k]["seconds"])
     t_min = levels[bound]["seconds"]
     return {"bound": bound, "t_min_s": t_min, "peak_GBps": bytes_per_launch / t_min / 1e9, "levels": levels,

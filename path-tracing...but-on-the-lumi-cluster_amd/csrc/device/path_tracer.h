@@ -223,6 +223,45 @@ struct LdsCold {
     }
 };
 
+// World ray and best hit all in registers, the best hit kept as LdsCold
+// keeps it (4 registers: thit is the walk's tmax).
+struct LeanCold {
+    f3 o, d;
+    float bu, bv;
+    uint32_t binst, bprim;     // bprim: primitive | back_face << 31
+
+    PTG_D void init(f3 ro, f3 rd, f3)
+    {
+        o = ro;
+        d = rd;
+        bu = bv = 0.0f;
+        binst = 0xFFFFFFFFu;
+        bprim = 0;
+    }
+    PTG_D f3 world_o() const { return o; }
+    PTG_D f3 world_d() const { return d; }
+    PTG_D void confirm(float u, float v, float, uint32_t instance, uint32_t prim, bool back)
+    {
+        bu = u;
+        bv = v;
+        binst = instance;
+        bprim = prim | (back ? 0x80000000u : 0u);
+    }
+    PTG_D Hit result(float tmax) const
+    {
+        const bool hit = binst != 0xFFFFFFFFu;
+        Hit h;
+        h.bx = bu;
+        h.by = bv;
+        h.bz = hit ? 1.0f - bu - bv : 0.0f;
+        h.thit = hit ? tmax : -1.0f;
+        h.instance_id = binst;
+        h.primitive_id = bprim & 0x7FFFFFFFu;
+        h.back_face = (bprim >> 31) != 0;
+        return h;
+    }
+};
+
 // Per-lane walk stacks of (word, near) entries (block_format.h: word = a
 // block index or kBeLeaf | payload; near = the entry distance, re-checked
 // against tmax when the entry is popped).
@@ -493,24 +532,24 @@ struct BlockWalker {
     PTG_D int node_step(const DevScene& sc, Counters& cnt)
     {
         if(cur == kBePop)
-        {
-            for(;;)
+        {   // one pop per node phase, straight-line: a culled entry or a
+            // finished BLAS simply costs the lane its next phase
+            if(st.size() == (axis < 0 ? 0u : bsp))
             {
-                if(st.size() == (axis < 0 ? 0u : bsp))
-                {
-                    if(axis < 0) return 1;
-                    if(pend != kBePop) return 0;   // its parked triangle needs this BLAS: wait for the leaf phase
-                    // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
-                    axis = -1;
-                    org = cold.world_o();
-                    inv = winv;
-                    fin = finite3(winv);
-                    oct = octant(cold.world_d());
-                    continue;
-                }
-                const uint2 e = st.pop();
-                if(__uint_as_float(e.y) < tmax) { cur = e.x; cnear = __uint_as_float(e.y); break; }   // the entry's test at its own time
+                if(axis < 0) return 1;
+                if(pend != kBePop) return 0;   // its parked triangle needs this BLAS: wait for the leaf phase
+                // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
+                axis = -1;
+                org = cold.world_o();
+                inv = winv;
+                fin = finite3(winv);
+                oct = octant(cold.world_d());
+                if(st.size() == 0) return 1;
             }
+            const uint2 e = st.pop();
+            if(!(__uint_as_float(e.y) < tmax)) return 0;   // the entry's test at its own time failed
+            cur = e.x;
+            cnear = __uint_as_float(e.y);
             if(cur & kBeLeaf)
             {
                 park();

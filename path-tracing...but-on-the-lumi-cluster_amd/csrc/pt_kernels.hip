@@ -224,6 +224,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WF_SLOTS
 #define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
 #endif
+#ifndef PTG_WALK_REGCOLD
+#define PTG_WALK_REGCOLD 0  // 1: the walk's world ray and best hit in registers, only the stack in LDS
+#endif
 #ifndef PTG_WALK_RESIDENT
 #define PTG_WALK_RESIDENT 4 // walk blocks per CU (LDS-bound with 16-entry stack windows: 4 x 40 KB)
 #endif
@@ -256,12 +259,20 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
+#if PTG_WALK_REGCOLD
+    // LDS: the stack windows, one 64-lane x kCap entry table per wave; the
+    // world ray and best hit stay in registers
+    extern __shared__ uint2 walk_lds[];
+    BlockWalker<LeanCold, LdsStack> w;
+    w.st.s = (lds_uint2_t*)(walk_lds + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);   // C cast: generic -> LDS
+#else
     // LDS: every lane's world ray, then the stack windows, one 64-lane x kCap
     // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
     BlockWalker<LdsCold, LdsStack> w;
     w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C casts: generic -> LDS address space
     w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);
+#endif
     w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
     bool active = false;
     uint32_t q = 0;
@@ -1244,7 +1255,7 @@ int ptg_context_create(int device, ptg_context** out)
     if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
-    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kCap);
+    const uint32_t lds_need = kBlock * uint32_t((PTG_WALK_REGCOLD ? 0 : sizeof(WalkCold)) + sizeof(uint2) * LdsStack::kCap);
     for(int k = 0; k < 2; ++k)
         ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / resident[k]) / 1024u * 1024u);
     int per_cu = 0;

@@ -6,8 +6,8 @@ tail -1 gpurun_out/parity.txt
 P=path-tracing...but-on-the-lumi-cluster_amd/_build
 for spec in "$@"; do
  lib=${spec%%:*}; envs=${spec#*:}
- for f in 450 0; do
-  for c in 0 2; do
+ for f in ${FR:-450 0}; do
+  for c in ${CC:-0 2}; do
    echo "== $lib [$envs] frame $f conc $c"
    env $envs PTG_LIB=$P/$lib timeout -k 10 200 python tools/ablate.py --spp 256 --frame $f --reps 2 --concurrency $c | grep -o '"wall_ms.*'
   done
