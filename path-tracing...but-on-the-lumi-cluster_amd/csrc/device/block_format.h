@@ -1,5 +1,5 @@
 // Block BVH records: the walk's traversal data, shared by the host packer
-// (host/block_bvh.cpp) and the device walker (device/block_walk.h).
+// (host/block_bvh.cpp) and the device walker (BlockWalker, device/path_tracer.h).
 //
 // The reference stores a BVH as nodes (bvh.hh:45-51, 24 B AABB) plus eight
 // stackless link orders (bvh.hh:53-67), one per ray-direction octant, and
@@ -30,28 +30,32 @@
 // Leaf boxes gate the triangle tests and BLAS entries, so they are always
 // decided at their own time (fact 2); inner boxes are tested only to prune.
 //
-// Layout.  The binary SAH tree (with multi-leaf buckets) is collapsed into
-// 4-wide blocks: a block holds up to four descendants of one node (its
-// children, some replaced by their own children).  A walk step loads one
-// block (128 B, eight 16-byte loads with no dependency between them), tests
-// all four boxes, continues with the first passing entry in the ray's order
-// and pushes the others onto a per-lane stack in reverse order.  Leaf
-// entries are pushed with their `near` and re-checked when popped; inner
-// entries are pushed bare (their subtree is entered and its own boxes tested
-// then, fact 1).  Leaves are thus met in the reference's order with the
-// reference's tmax: identical hits, ties and back-face flags.
+// Layout.  The binary SAH tree (with multi-leaf buckets, split into groups
+// of at most four) is collapsed into 4-wide blocks: a block holds up to four
+// descendants of one node (its children, some replaced by their own
+// children).  Each block is stored once per ray octant (8 x 4 entries): in
+// octant o's copy the entries are in the order a ray of that octant meets
+// them, and each box is stored as (near planes, far planes) for that
+// octant's direction signs, so with finite reciprocals the slab test needs no
+// per-axis min/max (t of the near plane is the reference's fmin(t0, t1) of
+// that axis, the far plane's its fmax).  A walk step loads one copy (128 B,
+// eight 16-byte loads with no dependency between them), tests all four
+// boxes, continues with the first passing entry and pushes the others, each
+// with its `near`, onto a per-lane stack in reverse order; a popped entry is
+// re-checked with `near < tmax` (fact 2).  Leaves are thus met in the
+// reference's order with the reference's tmax: identical hits, ties and
+// back-face flags.
 //
-//   BlockEntry (32 B)   lo.xyz | a   hi.xyz | b
+//   BlockEntry (32 B)   near.xyz | a   far.xyz | b
 //     a: kBeLeaf | payload   leaf (BLAS: triangle index in the mesh,
 //                            TLAS: instance index), payload < 2^28
-//        kBeNone             unused slot, never passes
+//        kBeNone             unused slot (NaN box, never passes)
 //        otherwise           block index of the child's own block
-//     b: slot order of the block: entry i holds octants 2i (bits 0-15) and
-//        2i+1 (bits 16-31); nibble j of an octant's half names the slot the
-//        ray meets j-th (unused slots last).
-// A BVH's handle is its root block's index.  One layout serves all eight
-// octants, so the records are ~13 MB for the 581k-node scene, against
-// 8 x 581k x 64 B = 298 MB of per-octant paired node records.
+//     b: unused (0)
+//   octant o's copy of block k: entries [(k * 8 + o) * 4, +4)
+// A BVH's handle is its root block's index; the root's own box is never
+// tested (fact 1).  The records are ~113 MB for the BLASes the animation
+// uses, against 8 x 581k x 64 B = 298 MB of per-octant paired node records.
 #pragma once
 #include <stdint.h>
 
