@@ -88,7 +88,8 @@ struct DevScene {
 #ifndef PTG_DEBUG
 #define PTG_DEBUG 0
 #endif
-enum : uint32_t { kDebugNode = 0, kDebugTri = 1, kDebugInst = 2, kDebugQueue = 3, kDebugList = 4, kDebugSlots = 8 };
+enum : uint32_t { kDebugNode = 0, kDebugTri = 1, kDebugInst = 2, kDebugQueue = 3, kDebugList = 4, kDebugStack = 5,
+                   kDebugSlots = 8 };
 
 // Aperture polygons with at most kPolyMaxSides sides read their vertex
 // directions from DevScene::polygon (k_polygon_table).

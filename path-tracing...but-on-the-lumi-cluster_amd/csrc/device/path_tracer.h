@@ -598,6 +598,8 @@ struct BlockWalker {
         const uint32_t rest = hits & (hits - 1u);
         if(rest)
         {   // written at the top either way, kept only if pushed
+            // (the host's stack bound, which sizes the spill areas, must hold)
+            PTG_CHECK(sc, st.size() + uint32_t(__builtin_popcount(rest)) <= sc.spill_stride, kDebugStack);
             st.reserve(kBlockWidth - 1);
             st.put(make_uint2(a3, __float_as_uint(n3)), (rest >> 3) & 1u);
             st.put(make_uint2(a2, __float_as_uint(n2)), (rest >> 2) & 1u);

@@ -1167,7 +1167,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipStreamSynchronize(ctx->stream));
         PTG_HIP(hipMemcpy(dbg, ctx->debug.p, sizeof(dbg), hipMemcpyDeviceToHost));
         std::string bad;
-        static const char* names[kDebugSlots] = {"node record", "triangle", "instance", "NEE list", "shade list", "", "", ""};
+        static const char* names[kDebugSlots] = {"node record", "triangle", "instance", "NEE list", "shade list", "walk stack", "", ""};
         for(uint32_t k = 0; k < kDebugSlots; ++k)
             if(dbg[k]) bad += std::string(bad.empty() ? "" : ", ") + names[k] + " index out of range x" + std::to_string(dbg[k]);
         if(!bad.empty())
