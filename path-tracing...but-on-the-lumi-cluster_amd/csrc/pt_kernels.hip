@@ -210,11 +210,11 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 #define PTG_REFILL_IDLE 24
 #endif
 constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many lanes are idle
-#ifdef PTG_WALK_WAVES
-#define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PTG_WALK_WAVES, 8)))
-#else
-#define PTG_WALK_ATTR
+#ifndef PTG_WALK_WAVES
+#define PTG_WALK_WAVES 5    // VGPR cap 96 (closest-hit walk: 104 uncapped, no spills at 96): the LDS holds 4 walk
+                            // blocks per CU, and the registers left beside them take a sky wave and more of shade
 #endif
+#define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PTG_WALK_WAVES, 8)))
 #ifndef PTG_WALK_UNROLL
 #define PTG_WALK_UNROLL 2   // node steps per leaf phase (block walker, 256 spp: 2 beats 1 by 1-3% and 3 by 2-5%, 4 is slower)
 #endif
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
 // (path_tracer.hh:456-588), retire.  No survivors.
 #ifndef PTG_SKY_WAVES
-#define PTG_SKY_WAVES 8     // 64 VGPRs: one sky wave fits beside 7 walk waves per SIMD (see ptg_context_create)
+#define PTG_SKY_WAVES 5     // 96 VGPRs, no spills (at 8 waves / 64 VGPRs it spilled 49): fits beside 4 walk waves per SIMD
 #endif
 #define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
 template<bool COUNT>
