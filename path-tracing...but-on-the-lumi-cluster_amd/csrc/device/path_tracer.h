@@ -611,45 +611,51 @@ struct BlockWalker {
 
     // Leaf phase: the parked triangle, else the BLAS entry or triangle the
     // walk stands at.  Returns 0, or 2 (ANY only) when a triangle occludes
-    // the ray.
+    // the ray.  Every lane's record - a triangle's TriRec (plus the next 16
+    // bytes) or an instance's InstTrav - is read by the same four loads before
+    // the kinds branch apart, so a wave with lanes of each kind waits for
+    // memory once per leaf phase.
     template<bool ANY, bool COUNT>
     PTG_D int leaf_step(const DevScene& sc, Counters& cnt)
     {
 #if PTG_PEND
-        if(pend != kBePop)
-        {
-            const uint32_t id = pend & kBeIndex;
-            const float n = pnear;
-            pend = kBePop;
-            if(n < tmax)   // the triangle's box test at its own time
-            {
-                if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
-                PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
-                const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + id);
-                if(const int r = tri_test<ANY>(id, tp[0], tp[1], tp[2])) return r;
-            }
-            park();   // a triangle waiting in cur is parked next
-            return 0;
-        }
+        const bool parked = pend != kBePop;
+#else
+        constexpr bool parked = false;
 #endif
-        const uint32_t id = cur & kBeIndex;
-        const float n = cnear;
-        cur = kBePop;
-        if(axis < 0)
+        const uint32_t id = (parked ? pend : cur) & kBeIndex;
+        const float n = parked ? pnear : cnear;
+        if(parked) pend = kBePop;
+        else cur = kBePop;
+        const bool inst_leaf = !parked && axis < 0;
+        // a triangle's box test at its own time (the walk re-checks near)
+        const bool tri = !inst_leaf && n < tmax;
+        if(inst_leaf) PTG_CHECK(sc, id < sc.inst_count, kDebugInst);
+        if(tri) PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
+        if(COUNT)
         {
-            PTG_CHECK(sc, id < sc.inst_count, kDebugInst);
-            if(COUNT) { cnt.blas_entries++; cnt.step_loads |= 4u; }
-            // whole-row vector loads: float4 members get re-split by the
-            // compiler into unaligned pieces (5 loads instead of 4)
-            const v4f* ip = reinterpret_cast<const v4f*>(sc.inst_trav + id);
-            enter(id, ip[0], ip[1], ip[2], ip[3]);
+            if(inst_leaf) { cnt.blas_entries++; cnt.step_loads |= 4u; }
+            if(tri) { cnt.tri_tests++; cnt.step_loads |= 2u; }
+        }
+        // whole-row vector loads (the tris buffer has 64 bytes of slack)
+        const v4f* p = inst_leaf ? reinterpret_cast<const v4f*>(sc.inst_trav + id)
+                                 : reinterpret_cast<const v4f*>(sc.tris + tri_base + id);
+        v4f r0 = {0, 0, 0, 0}, r1 = r0, r2 = r0, r3 = r0;
+        if(inst_leaf || tri)
+        {
+            r0 = p[0]; r1 = p[1]; r2 = p[2]; r3 = p[3];
+        }
+        if(inst_leaf)
+        {
+            enter(id, r0, r1, r2, r3);
             return 0;
         }
-        if(!(n < tmax)) return 0;   // re-checked at its own time (a triangle reached behind a parked one)
-        if(COUNT) { cnt.tri_tests++; cnt.step_loads |= 2u; }
-        PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
-        const float4* tp = reinterpret_cast<const float4*>(sc.tris + tri_base + id);
-        return tri_test<ANY>(id, tp[0], tp[1], tp[2]);
+        if(tri)
+            if(const int r = tri_test<ANY>(id, make_float4(r0.x, r0.y, r0.z, r0.w), make_float4(r1.x, r1.y, r1.z, r1.w),
+                                           make_float4(r2.x, r2.y, r2.z, r2.w)))
+                return r;
+        if(parked) park();   // a triangle waiting in cur is parked next
+        return 0;
     }
 
     // One step of either phase (the per-lane walks: the megakernel and the
