@@ -712,6 +712,35 @@ struct DevBuf {
     template<typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned host staging for asynchronous uploads; `done` marks the end of the
+// copies that last read it.
+struct HostStage {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+    ~HostStage()
+    {
+        if(done)
+        {
+            (void)hipEventSynchronize(done);
+            (void)hipEventDestroy(done);
+        }
+        if(p) (void)hipHostFree(p);
+    }
+    // waits for the copies that last read it, then grows it to n bytes
+    hipError_t reserve(size_t n)
+    {
+        if(!done)
+            if(hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming)) return e;
+        if(hipError_t e = hipEventSynchronize(done)) return e;
+        if(n <= bytes && p) return hipSuccess;
+        if(p) { (void)hipHostFree(p); p = nullptr; bytes = 0; }
+        hipError_t e = hipHostMalloc(&p, std::max<size_t>(n, 1), hipHostMallocDefault);
+        if(e == hipSuccess) bytes = std::max<size_t>(n, 1);
+        return e;
+    }
+};
+
 int hip_fail(hipError_t e, const char* what)
 {
     set_last_error(std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
@@ -752,6 +781,8 @@ struct ptg_context {
     bool scene_ready = false;
     // frame: blocks = [BLAS blocks][this frame's TLAS blocks]
     DevBuf blocks, tlas_root, subframes, inst_trav, inst_shade, jobs, polygon, spill;
+    HostStage stage[2];                                  // ptg_upload_frame's pinned staging, used alternately
+    uint32_t stage_next = 0;
     size_t block_count = 0, subframe_count = 0, instance_count = 0;
     uint32_t stack_bound = 0;                            // TLAS + BLAS stack bound of this frame (entries)
     std::vector<uint32_t> host_tlas_root;
@@ -1420,41 +1451,72 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
             mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
     }
 
-    // device copies: blocks = [BLAS blocks][TLAS blocks]; growing the buffer
-    // drops the BLAS blocks already there, which are then uploaded again
+    // Device copies, asynchronous: everything the frame uploads is gathered
+    // into one of two pinned staging buffers and copied on the context's
+    // stream, behind the render already queued there - the host returns at
+    // once and the next render queues right behind the copies.  A staging
+    // buffer is reused only after its copies of two uploads ago completed.
+    // Growing a device buffer frees the old one, which an in-flight render
+    // may still read: the stream is drained first (rare).
+    bool drained = false;
+    auto grow = [&](DevBuf& b, size_t n) -> hipError_t {
+        if(n <= b.bytes && b.p) return hipSuccess;
+        if(!drained)
+        {
+            if(hipError_t e = hipStreamSynchronize(s)) return e;
+            drained = true;
+        }
+        return b.reserve(n);
+    };
+    // blocks = [BLAS blocks][TLAS blocks]; growing the buffer drops the BLAS
+    // blocks already there, which are then uploaded again
     const std::vector<BlockEntry>& old_blas = ctx->cache.blas;
     const size_t blas_total = old_blas.size() + fp.new_blas.size();
     const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockEntry);
     if(need > ctx->blocks.bytes)
     {
-        PTG_HIP(hipStreamSynchronize(s));
+        PTG_HIP(grow(ctx->blocks, need + need / 8));
         ctx->blas_on_device = 0;
-        PTG_HIP(ctx->blocks.reserve(need + need / 8));
     }
+    PTG_HIP(grow(ctx->tlas_root, subframe_count * sizeof(uint32_t)));
+    PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav)));
+    PTG_HIP(grow(ctx->inst_shade, instance_count * sizeof(InstShade)));
+    PTG_HIP(grow(ctx->subframes, subframe_count * sizeof(ptg_subframe)));
+    PTG_HIP(grow(ctx->polygon, subframe_count * kPolyStride * sizeof(float2)));
+    if(!mesh_jobs.empty()) PTG_HIP(grow(ctx->jobs, mesh_jobs.size() * sizeof(MeshJob)));
     BlockEntry* dev = ctx->blocks.as<BlockEntry>();
+    struct Part { const void* src; size_t n; void* dst; };
+    std::vector<Part> parts;
     if(ctx->blas_on_device < old_blas.size())
-        PTG_HIP(hipMemcpyAsync(dev + ctx->blas_on_device, old_blas.data() + ctx->blas_on_device,
-                               (old_blas.size() - ctx->blas_on_device) * sizeof(BlockEntry), hipMemcpyHostToDevice, s));
-    if(!fp.new_blas.empty())
-        PTG_HIP(hipMemcpyAsync(dev + old_blas.size(), fp.new_blas.data(), fp.new_blas.size() * sizeof(BlockEntry),
-                               hipMemcpyHostToDevice, s));
-    PTG_HIP(hipMemcpyAsync(dev + blas_total, fp.tlas.data(), fp.tlas.size() * sizeof(BlockEntry), hipMemcpyHostToDevice, s));
-    PTG_HIP(ctx->tlas_root.reserve(subframe_count * sizeof(uint32_t)));
-    PTG_HIP(hipMemcpyAsync(ctx->tlas_root.p, fp.tlas_root.data(), subframe_count * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    PTG_HIP(ctx->inst_trav.reserve(instance_count * sizeof(InstTrav)));
-    PTG_HIP(ctx->inst_shade.reserve(instance_count * sizeof(InstShade)));
-    PTG_HIP(ctx->subframes.reserve(subframe_count * sizeof(ptg_subframe)));
-    PTG_HIP(hipMemcpyAsync(ctx->inst_trav.p, it.data(), instance_count * sizeof(InstTrav), hipMemcpyHostToDevice, s));
-    PTG_HIP(hipMemcpyAsync(ctx->inst_shade.p, is.data(), instance_count * sizeof(InstShade), hipMemcpyHostToDevice, s));
-    PTG_HIP(hipMemcpyAsync(ctx->subframes.p, subframes, subframe_count * sizeof(ptg_subframe), hipMemcpyHostToDevice, s));
-    PTG_HIP(ctx->polygon.reserve(subframe_count * kPolyStride * sizeof(float2)));
+        parts.push_back({old_blas.data() + ctx->blas_on_device, (old_blas.size() - ctx->blas_on_device) * sizeof(BlockEntry),
+                         dev + ctx->blas_on_device});
+    parts.push_back({fp.new_blas.data(), fp.new_blas.size() * sizeof(BlockEntry), dev + old_blas.size()});
+    parts.push_back({fp.tlas.data(), fp.tlas.size() * sizeof(BlockEntry), dev + blas_total});
+    parts.push_back({fp.tlas_root.data(), subframe_count * sizeof(uint32_t), ctx->tlas_root.p});
+    parts.push_back({it.data(), instance_count * sizeof(InstTrav), ctx->inst_trav.p});
+    parts.push_back({is.data(), instance_count * sizeof(InstShade), ctx->inst_shade.p});
+    parts.push_back({subframes, subframe_count * sizeof(ptg_subframe), ctx->subframes.p});
+    parts.push_back({mesh_jobs.data(), mesh_jobs.size() * sizeof(MeshJob), ctx->jobs.p});
+    size_t total = 0;
+    for(const Part& q: parts) total += (q.n + 255) & ~size_t(255);
+    HostStage& hs = ctx->stage[ctx->stage_next];
+    ctx->stage_next ^= 1u;
+    PTG_HIP(hs.reserve(total));
+    size_t off = 0;
+    for(const Part& q: parts)
+    {
+        if(q.n == 0) continue;
+        char* h = static_cast<char*>(hs.p) + off;
+        memcpy(h, q.src, q.n);
+        PTG_HIP(hipMemcpyAsync(q.dst, h, q.n, hipMemcpyHostToDevice, s));
+        off += (q.n + 255) & ~size_t(255);
+    }
+    PTG_HIP(hipEventRecord(hs.done, s));
     hipLaunchKernelGGL(k_polygon_table, dim3(grid_for(subframe_count * kPolyStride)), dim3(kBlock), 0, s,
                        ctx->subframes.as<uint8_t>(), uint32_t(subframe_count), ctx->polygon.as<float2>());
     PTG_HIP(hipGetLastError());
     if(!mesh_jobs.empty())
     {
-        PTG_HIP(ctx->jobs.reserve(mesh_jobs.size() * sizeof(MeshJob)));
-        PTG_HIP(hipMemcpyAsync(ctx->jobs.p, mesh_jobs.data(), mesh_jobs.size() * sizeof(MeshJob), hipMemcpyHostToDevice, s));
         uint32_t maxt = 0;
         for(const MeshJob& j: mesh_jobs) maxt = std::max(maxt, j.triangle_count);
         dim3 grid(std::min<uint32_t>(grid_for(maxt), 4096), uint32_t(mesh_jobs.size()));
@@ -1462,7 +1524,6 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
                            ctx->tris.as<TriRec>(), ctx->jobs.as<MeshJob>());
         PTG_HIP(hipGetLastError());
     }
-    PTG_HIP(hipStreamSynchronize(s));   // the host vectors above are released on return
 
     // commit
     ctx->cache.commit(fp);
