@@ -214,7 +214,10 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #define PTG_WALK_WAVES 5    // VGPR cap 96 (closest-hit walk: 104 uncapped, no spills at 96): the LDS holds 4 walk
                             // blocks per CU, and the registers left beside them take a sky wave and more of shade
 #endif
-#define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PTG_WALK_WAVES, 8)))
+#ifndef PTG_SHADOW_WAVES
+#define PTG_SHADOW_WAVES 6  // the any-hit walk fits 80 VGPRs without spills (76): a shade wave (160) fits beside it
+#endif
+#define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(ANY ? PTG_SHADOW_WAVES : PTG_WALK_WAVES, 8)))
 #ifndef PTG_WALK_UNROLL
 #define PTG_WALK_UNROLL 2   // node steps per leaf phase (block walker, 256 spp: 2 beats 1 by 1-3% and 3 by 2-5%, 4 is slower)
 #endif
