@@ -166,7 +166,11 @@ int ptg_upload_scene(ptg_context* ctx,
  * first_node .. first_node+frame_node_count-1 of the reference's
  * bvh_buffers; first_node must equal the static node count).  instances is
  * the full instance array (static + this frame's dynamic ones).  Host
- * pointers. */
+ * pointers, read before the call returns (the caller may overwrite them at
+ * once); the device copies are queued on the context's stream behind any
+ * render already queued there.  The call waits only for the copies of the
+ * upload two calls back (its pinned staging is reused) or, when a device
+ * buffer must grow, for the stream to drain. */
 int ptg_upload_frame(ptg_context* ctx,
                      const ptg_subframe* subframes, size_t subframe_count,
                      const ptg_tlas_instance* instances, size_t instance_count,
