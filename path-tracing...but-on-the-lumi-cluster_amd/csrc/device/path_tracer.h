@@ -525,11 +525,10 @@ struct BlockWalker {
 #endif
     }
 
-    // Node phase: pop the next entry if the walk needs one, then, if it is a
-    // block, one block step.  Returns 1 when the walk has ended, else 0 (the
-    // walk may then stand at a leaf, which leaf_step() takes).
-    template<bool COUNT>
-    PTG_D int node_step(const DevScene& sc, Counters& cnt)
+    // Node phase, first half: pop the next entry if the walk needs one.
+    // Returns -1 when cur is a block to step now, else what node_step returns
+    // (0: nothing to step this phase, 1: the walk has ended).
+    PTG_D int node_pop()
     {
         if(cur == kBePop)
         {   // one pop per node phase, straight-line: a culled entry or a
@@ -556,13 +555,22 @@ struct BlockWalker {
                 return 0;
             }
         }
-        const uint32_t w = cur;
-        PTG_CHECK(sc, w < sc.block_count, kDebugNode);
-        // this octant's copy of the block: its four entries in the order the
-        // ray meets them, each box as (near planes, far planes) for the
-        // octant's signs; eight independent 16-byte loads
-        const v4f* p = reinterpret_cast<const v4f*>(sc.blocks + (size_t(w) * 8u + oct) * kBlockWidth);
-        const v4f q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4], q5 = p[5], q6 = p[6], q7 = p[7];
+        return -1;
+    }
+
+    // this octant's copy of block cur: its four entries in the order the ray
+    // meets them, each box as (near planes, far planes) for the octant's
+    // signs; eight 16-byte rows
+    PTG_D const v4f* block_rows(const DevScene& sc) const
+    {
+        return reinterpret_cast<const v4f*>(sc.blocks + (size_t(cur) * 8u + oct) * kBlockWidth);
+    }
+
+    // Node phase, second half: the block step on its eight rows.
+    template<bool COUNT>
+    PTG_D int node_block(const DevScene& sc, Counters& cnt, v4f q0, v4f q1, v4f q2, v4f q3, v4f q4, v4f q5, v4f q6,
+                         v4f q7)
+    {
         const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q1.x, q1.y, q1.z, q1.w);
         const float4 l1 = make_float4(q2.x, q2.y, q2.z, q2.w), h1 = make_float4(q3.x, q3.y, q3.z, q3.w);
         const float4 l2 = make_float4(q4.x, q4.y, q4.z, q4.w), h2 = make_float4(q5.x, q5.y, q5.z, q5.w);
@@ -609,6 +617,67 @@ struct BlockWalker {
         return 0;
     }
 
+    // Node phase: pop the next entry if the walk needs one, then, if it is a
+    // block, one block step.  Returns 1 when the walk has ended, else 0 (the
+    // walk may then stand at a leaf, which leaf_step() takes).
+    template<bool COUNT>
+    PTG_D int node_step(const DevScene& sc, Counters& cnt)
+    {
+        if(const int r = node_pop(); r >= 0) return r;
+        PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
+        const v4f* p = block_rows(sc);
+        return node_block<COUNT>(sc, cnt, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+    }
+
+    // Leaf phase, first half: the parked triangle, else the BLAS entry or
+    // triangle the walk stands at; its record's rows and whether it is
+    // tested (a triangle's box test at its own time: the walk re-checks near).
+    struct LeafSel {
+        const v4f* p;
+        uint32_t id;
+        bool parked, inst_leaf, tri;
+    };
+    PTG_D LeafSel leaf_select(const DevScene& sc)
+    {
+        LeafSel ls;
+#if PTG_PEND
+        ls.parked = pend != kBePop;
+#else
+        ls.parked = false;
+#endif
+        ls.id = (ls.parked ? pend : cur) & kBeIndex;
+        const float n = ls.parked ? pnear : cnear;
+        if(ls.parked) pend = kBePop;
+        else cur = kBePop;
+        ls.inst_leaf = !ls.parked && axis < 0;
+        ls.tri = !ls.inst_leaf && n < tmax;
+        ls.p = ls.inst_leaf ? reinterpret_cast<const v4f*>(sc.inst_trav + ls.id)
+                            : reinterpret_cast<const v4f*>(sc.tris + tri_base + ls.id);
+        return ls;
+    }
+
+    // Leaf phase, second half, on the record's first four rows.
+    template<bool ANY, bool COUNT>
+    PTG_D int leaf_finish(const DevScene& sc, Counters& cnt, const LeafSel& ls, v4f r0, v4f r1, v4f r2, v4f r3)
+    {
+        if(COUNT)
+        {
+            if(ls.inst_leaf) { cnt.blas_entries++; cnt.step_loads |= 4u; }
+            if(ls.tri) { cnt.tri_tests++; cnt.step_loads |= 2u; }
+        }
+        if(ls.inst_leaf)
+        {
+            enter(ls.id, r0, r1, r2, r3);
+            return 0;
+        }
+        if(ls.tri)
+            if(const int r = tri_test<ANY>(ls.id, make_float4(r0.x, r0.y, r0.z, r0.w), make_float4(r1.x, r1.y, r1.z, r1.w),
+                                           make_float4(r2.x, r2.y, r2.z, r2.w)))
+                return r;
+        if(ls.parked) park();   // a triangle waiting in cur is parked next
+        return 0;
+    }
+
     // Leaf phase: the parked triangle, else the BLAS entry or triangle the
     // walk stands at.  Returns 0, or 2 (ANY only) when a triangle occludes
     // the ray.  Every lane's record - a triangle's TriRec (plus the next 16
@@ -618,44 +687,56 @@ struct BlockWalker {
     template<bool ANY, bool COUNT>
     PTG_D int leaf_step(const DevScene& sc, Counters& cnt)
     {
-#if PTG_PEND
-        const bool parked = pend != kBePop;
-#else
-        constexpr bool parked = false;
-#endif
-        const uint32_t id = (parked ? pend : cur) & kBeIndex;
-        const float n = parked ? pnear : cnear;
-        if(parked) pend = kBePop;
-        else cur = kBePop;
-        const bool inst_leaf = !parked && axis < 0;
-        // a triangle's box test at its own time (the walk re-checks near)
-        const bool tri = !inst_leaf && n < tmax;
-        if(inst_leaf) PTG_CHECK(sc, id < sc.inst_count, kDebugInst);
-        if(tri) PTG_CHECK(sc, tri_base + id < sc.tri_count, kDebugTri);
-        if(COUNT)
-        {
-            if(inst_leaf) { cnt.blas_entries++; cnt.step_loads |= 4u; }
-            if(tri) { cnt.tri_tests++; cnt.step_loads |= 2u; }
-        }
-        // whole-row vector loads (the tris buffer has 64 bytes of slack)
-        const v4f* p = inst_leaf ? reinterpret_cast<const v4f*>(sc.inst_trav + id)
-                                 : reinterpret_cast<const v4f*>(sc.tris + tri_base + id);
+        const LeafSel ls = leaf_select(sc);
+        if(ls.inst_leaf) PTG_CHECK(sc, ls.id < sc.inst_count, kDebugInst);
+        if(ls.tri) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);
         v4f r0 = {0, 0, 0, 0}, r1 = r0, r2 = r0, r3 = r0;
-        if(inst_leaf || tri)
+        if(ls.inst_leaf || ls.tri)
         {
-            r0 = p[0]; r1 = p[1]; r2 = p[2]; r3 = p[3];
+            r0 = ls.p[0]; r1 = ls.p[1]; r2 = ls.p[2]; r3 = ls.p[3];
         }
-        if(inst_leaf)
+        return leaf_finish<ANY, COUNT>(sc, cnt, ls, r0, r1, r2, r3);
+    }
+
+    // PTG_WALK_SCHED 1: one step of either kind - the lane's leaf work if it
+    // has any, else a node step - with both kinds' rows read by the same
+    // eight loads (a leaf lane's last four rows are unused; the record
+    // buffers carry the slack), so a wave with lanes of both kinds waits for
+    // memory once.  Returns as node_step / leaf_step.
+    template<bool ANY, bool COUNT>
+    PTG_D int mixed_step(const DevScene& sc, Counters& cnt)
+    {
+        const bool lf = wants_leaf();
+        LeafSel ls{nullptr, 0, false, false, false};
+        int nr = -1;
+        const v4f* p = nullptr;
+        bool load;
+        if(lf)
         {
-            enter(id, r0, r1, r2, r3);
-            return 0;
+            ls = leaf_select(sc);
+            if(ls.inst_leaf) PTG_CHECK(sc, ls.id < sc.inst_count, kDebugInst);
+            if(ls.tri) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);
+            p = ls.p;
+            load = ls.inst_leaf || ls.tri;
         }
-        if(tri)
-            if(const int r = tri_test<ANY>(id, make_float4(r0.x, r0.y, r0.z, r0.w), make_float4(r1.x, r1.y, r1.z, r1.w),
-                                           make_float4(r2.x, r2.y, r2.z, r2.w)))
-                return r;
-        if(parked) park();   // a triangle waiting in cur is parked next
-        return 0;
+        else
+        {
+            nr = node_pop();
+            load = nr < 0;
+            if(load)
+            {
+                PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
+                p = block_rows(sc);
+            }
+        }
+        v4f q0 = {0, 0, 0, 0}, q1 = q0, q2 = q0, q3 = q0, q4 = q0, q5 = q0, q6 = q0, q7 = q0;
+        if(load)
+        {
+            q0 = p[0]; q1 = p[1]; q2 = p[2]; q3 = p[3]; q4 = p[4]; q5 = p[5]; q6 = p[6]; q7 = p[7];
+        }
+        if(lf) return leaf_finish<ANY, COUNT>(sc, cnt, ls, q0, q1, q2, q3);
+        if(nr >= 0) return nr;
+        return node_block<COUNT>(sc, cnt, q0, q1, q2, q3, q4, q5, q6, q7);
     }
 
     // One step of either phase (the per-lane walks: the megakernel and the

@@ -221,6 +221,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WALK_UNROLL
 #define PTG_WALK_UNROLL 2   // node steps per leaf phase (block walker, 256 spp: 2 beats 1 by 1-3% and 3 by 2-5%, 4 is slower)
 #endif
+#ifndef PTG_WALK_SCHED
+#define PTG_WALK_SCHED 0    // 0: node phases then a leaf phase; 1: a step of either kind, then a node step (slower, kept as an option)
+#endif
 #ifndef PTG_VMEM_STATS
 #define PTG_VMEM_STATS 0
 #endif
@@ -355,6 +358,20 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
         // lanes that are.  The leaf code (triangle test, BLAS entry) then runs
         // once per iteration with many lanes, not once per block step with few.
         int r = 0;
+#if PTG_WALK_SCHED == 1
+        // a step of either kind (leaf work first), then a node step
+        if(active)
+        {
+            r = w.template mixed_step<ANY, COUNT>(sc, cnt);
+            if(r != 0) { finish(r); active = false; r = 0; }
+        }
+        if(active && !w.at_leaf())
+        {
+            r = w.template node_step<COUNT>(sc, cnt);
+            if(r != 0) { finish(r); active = false; }
+        }
+        continue;
+#endif
 #pragma unroll
         for(int u = 0; u < PTG_WALK_UNROLL; ++u)
         {
@@ -1390,8 +1407,9 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     PTG_HIP(ctx->normal.reserve(vertex_count * 16));
     PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
     PTG_HIP(ctx->material.reserve(vertex_count * 16));
-    // one 16 B record of slack: the walk reads a triangle as four 16-byte rows
-    PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 64));
+    // 128 bytes of slack: the walk reads a triangle as four (a mixed step:
+    // eight) 16-byte rows
+    PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 128));
     hipStream_t s = ctx->stream;
     PTG_HIP(hipMemcpyAsync(ctx->indices.p, indices, index_count * 4, hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->pos.p, pos, vertex_count * 16, hipMemcpyHostToDevice, s));
@@ -1482,7 +1500,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
         ctx->blas_on_device = 0;
     }
     PTG_HIP(grow(ctx->tlas_root, subframe_count * sizeof(uint32_t)));
-    PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav)));
+    PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav) + 64));   // slack: a mixed walk step reads 8 rows
     PTG_HIP(grow(ctx->inst_shade, instance_count * sizeof(InstShade)));
     PTG_HIP(grow(ctx->subframes, subframe_count * sizeof(ptg_subframe)));
     PTG_HIP(grow(ctx->polygon, subframe_count * kPolyStride * sizeof(float2)));
