@@ -4,6 +4,7 @@
 #include "block_bvh.h"
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <unordered_map>
 #include <cmath>
 #include <limits>
@@ -59,6 +60,7 @@ bool derive(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count
             continue;
         }
         uint32_t c = l7.accept;
+        t.kids[n].reserve(2);
         for(;;)
         {
             if(c >= count || c == 0) { err = "link outside the BVH"; return false; }
@@ -225,6 +227,7 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
         for(uint32_t o = 0; o < 8; ++o)
         {
             std::vector<uint32_t> seq;
+            seq.reserve(W);
             auto walk = [&](auto&& self, uint32_t n) -> void {
                 const std::vector<uint32_t>& ks = t.kids[n];
                 const bool rev = ((o >> t.axis[n]) & 1u) == 0;
@@ -285,9 +288,15 @@ static void dedup_tlas(FramePack& fp)
         memcpy(tmp, &fp.tlas[k * E], sizeof(tmp));
         for(BlockEntry& e: tmp)
             if(!(e.a & (kBeLeaf | kBeNone))) e.a = canon[e.a - fp.tlas_base];
-        uint64_t h = 1469598103934665603ull;   // FNV-1a over the block's bytes
-        const unsigned char* b = reinterpret_cast<const unsigned char*>(tmp);
-        for(size_t i = 0; i < sizeof(tmp); ++i) h = (h ^ b[i]) * 1099511628211ull;
+        uint64_t h = 1469598103934665603ull;   // FNV-style mix over the block's 64-bit words
+        static_assert(sizeof(tmp) % 8 == 0, "whole words");
+        for(size_t i = 0; i < sizeof(tmp); i += 8)
+        {
+            uint64_t w;
+            memcpy(&w, reinterpret_cast<const unsigned char*>(tmp) + i, 8);
+            h = (h ^ w) * 1099511628211ull;
+            h ^= h >> 29;
+        }
         std::vector<uint32_t>& bucket = table[h];
         uint32_t id = 0xFFFFFFFFu;
         for(uint32_t c: bucket)
@@ -372,14 +381,51 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
         if(t.node_offset < first_node || uint64_t(t.node_offset) + t.node_count > first_node + frame_node_count ||
            t.node_count == 0)
         { err = "subframe " + std::to_string(i) + ": TLAS outside the frame nodes"; return PTG_E_RANGE; }
-        const size_t rel = t.node_offset - first_node;
-        BlockBvh info;
-        // every TLAS leaf must name a valid instance
-        if(!pack_block_bvh(frame_nodes + rel, frame_links + 8 * rel, t.node_count, fp.tlas_base, uint32_t(instance_count),
-                           fp.tlas, info, why))
-        { err = "subframe " + std::to_string(i) + ": TLAS: " + why; return PTG_E_RANGE; }
-        fp.tlas_root[i] = info.root;
-        fp.tlas_stack = std::max(fp.tlas_stack, info.stack_entries);
+    }
+    // The subframes' TLASes are independent: packed on several host threads,
+    // each at block base 0, then laid out one after another and relocated.
+    std::vector<std::vector<BlockEntry>> part(subframe_count);
+    std::vector<BlockBvh> pinfo(subframe_count);
+    std::vector<std::string> perr(subframe_count);
+    std::vector<char> pok(subframe_count, 0);
+    auto pack_range = [&](size_t i0, size_t i1) {
+        for(size_t i = i0; i < i1; ++i)
+        {
+            const ptg_bvh& t = subframes[i].tlas;
+            const size_t rel = t.node_offset - first_node;
+            // every TLAS leaf must name a valid instance
+            pok[i] = pack_block_bvh(frame_nodes + rel, frame_links + 8 * rel, t.node_count, 0, uint32_t(instance_count),
+                                    part[i], pinfo[i], perr[i]);
+        }
+    };
+    const size_t nthreads = std::min<size_t>(subframe_count, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+    if(nthreads > 1)
+    {
+        std::vector<std::thread> pool;
+        for(size_t k = 0; k < nthreads; ++k)
+            pool.emplace_back(pack_range, subframe_count * k / nthreads, subframe_count * (k + 1) / nthreads);
+        for(std::thread& th: pool) th.join();
+    }
+    else
+        pack_range(0, subframe_count);
+    size_t total_entries = 0;
+    for(size_t i = 0; i < subframe_count; ++i)
+    {
+        if(!pok[i]) { err = "subframe " + std::to_string(i) + ": TLAS: " + perr[i]; return PTG_E_RANGE; }
+        total_entries += part[i].size();
+    }
+    fp.tlas.reserve(total_entries);
+    for(size_t i = 0; i < subframe_count; ++i)
+    {
+        const uint32_t base = fp.tlas_base + uint32_t(fp.tlas.size() / kBlockEntries);
+        if(uint64_t(base) + part[i].size() / kBlockEntries > kBeIndex) { err = "TLAS records above 2^28 blocks"; return PTG_E_RANGE; }
+        for(BlockEntry e: part[i])
+        {
+            if(!(e.a & (kBeLeaf | kBeNone))) e.a += base;
+            fp.tlas.push_back(e);
+        }
+        fp.tlas_root[i] = pinfo[i].root + base;
+        fp.tlas_stack = std::max(fp.tlas_stack, pinfo[i].stack_entries);
     }
     dedup_tlas(fp);
     // every block index a walk can follow lies inside the buffer (the

@@ -16,6 +16,7 @@
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/block_bvh.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/hmath.h"
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -331,12 +332,21 @@ Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats&
 {
     st.queries++;
     SimWalker w(v, pk, q, st, C, g_spec);
+    static const int sched = getenv("SCHED") ? atoi(getenv("SCHED")) : 0;
     for(;;)
     {
         int r = 0;
-        for(int u = 0; u < 2 && r == 0; ++u)
-            if(!w.at_leaf()) r = w.node_step();
-        if(r == 0 && w.wants_leaf()) r = w.leaf_step();
+        if(sched == 1)
+        {   // experiment: [mixed phase: leaf work if any, else a node step] + [node phase]
+            r = w.wants_leaf() ? w.leaf_step() : w.node_step();
+            if(r == 0 && !w.at_leaf()) r = w.node_step();
+        }
+        else
+        {
+            for(int u = 0; u < 2 && r == 0; ++u)
+                if(!w.at_leaf()) r = w.node_step();
+            if(r == 0 && w.wants_leaf()) r = w.leaf_step();
+        }
         if(r) break;
         st.iters++;
     }
@@ -389,7 +399,21 @@ int main(int argc, char** argv)
         if(ptg_scene_setup_frame(scene, frame)) { fprintf(stderr, "%s\n", ptg_last_error()); return 1; }
         ptg_scene_view_get(scene, &v);
     }
+    const auto tp0 = std::chrono::steady_clock::now();
     if(pack()) { fprintf(stderr, "frame %u: %s\n", frame, err.c_str()); return 1; }
+    printf("pack_frame %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count());
+    if(getenv("PACKTIME"))
+    {   // steady state: the same frame again with its BLASes committed (TLASes only)
+        FramePack keep = fp;
+        cache.commit(fp);
+        for(int k = 0; k < 3; ++k)
+        {
+            const auto t1 = std::chrono::steady_clock::now();
+            if(pack()) return 1;
+            printf("pack_frame again %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+        }
+        return 0;
+    }
     Packed pk;
     pk.E = cache.blas;
     pk.E.insert(pk.E.end(), fp.new_blas.begin(), fp.new_blas.end());
