@@ -23,6 +23,8 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
+#include <set>
 #include <vector>
 
 using namespace ptg;
@@ -175,6 +177,8 @@ constexpr uint32_t POP = 0xFFFFFFFFu;
 
 // ---- block walk (production packer, device algorithm) -----------------------
 bool g_spec = true;   // SPEC=0: no parked triangles
+std::set<uint64_t>* g_visits = nullptr;   // PACKET=1: the (instance, block) pairs a query steps
+uint64_t g_last_block = ~0ull;              // the (instance, block) pair the last node step stepped
 
 struct Packed {
     std::vector<BlockEntry> E;         // the device block buffer: [BLAS blocks][TLAS blocks]
@@ -248,6 +252,8 @@ struct SimWalker {
         st.steps++;
         st.block_steps++;
         st.bytes += 128;
+        if(g_visits) g_visits->insert((uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur);
+        g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur;
         // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
         const BlockEntry* e = &pk.E[(size_t(cur) * 8u + octant(dir)) * kBlockWidth];
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
@@ -423,6 +429,91 @@ int main(int argc, char** argv)
     printf("frame %u: BLAS %zu + %zu new entries (%.1f MB), TLAS %zu entries (%.1f MB); stack bound %u entries (TLAS %u)\n",
            frame, cache.blas.size(), fp.new_blas.size(), (cache.blas.size() + fp.new_blas.size()) * 32 / 1e6, fp.tlas.size(),
            fp.tlas.size() * 32 / 1e6, fp.stack_bound(), fp.tlas_stack);
+
+    if(getenv("PACKET"))
+    {   // how much a wave of camera rays (8 pixels x 8 jittered samples, one
+        // subframe) shares: the union of the blocks its lanes step
+        double lane_steps = 0, union_steps = 0, groups = 0;
+        for(int g = 0; g < 400; ++g)
+        {
+            const uint32_t px0 = uint32_t(rnd() * (cfg.width / 8)) * 8, py = uint32_t(rnd() * cfg.height);
+            const uint32_t sf = uint32_t(rnd() * v.subframe_count) % v.subframe_count;
+            const ptg_camera& cam = v.subframes[sf].cam;
+            std::set<uint64_t> uni;
+            for(int l = 0; l < 64; ++l)
+            {
+                const float fx = px0 + (l >> 3) + rnd(), fy = py + rnd();
+                float ux = fx / cfg.width * 2.0f - 1.0f, uy = fy / cfg.height * 2.0f - 1.0f;
+                ux *= cam.aspect_ratio;
+                uy = -uy;
+                f3 d = normalize(v3(ux * cam.inv_focal_length, uy * cam.inv_focal_length, -1.0f));
+                d = mul_m3v3(cam.orientation, d);
+                std::set<uint64_t> mine;
+                g_visits = &mine;
+                Stats tmp;
+                block_walk(v, pk, Query{cam.position, d, 0.0f, 1e9f, sf, false}, tmp, S);
+                g_visits = nullptr;
+                lane_steps += double(mine.size());
+                uni.insert(mine.begin(), mine.end());
+            }
+            union_steps += double(uni.size());
+            groups += 1;
+        }
+        printf("camera-ray waves: %.1f block steps per lane, %.1f in the union of a wave's 64 lanes\n", lane_steps / groups / 64,
+               union_steps / groups);
+        // the device's lockstep schedule (2 node phases, 1 leaf phase) for such waves: how many node
+        // phases have every stepping lane on the same block
+        double phases = 0, uniform = 0, distinct = 0, iters = 0;
+        for(int g = 0; g < 200; ++g)
+        {
+            const uint32_t px0 = uint32_t(rnd() * (cfg.width / 8)) * 8, py = uint32_t(rnd() * cfg.height);
+            const uint32_t sf = uint32_t(rnd() * v.subframe_count) % v.subframe_count;
+            const ptg_camera& cam = v.subframes[sf].cam;
+            std::vector<Query> wq(64);
+            std::vector<Stats> wst(64);
+            std::vector<std::unique_ptr<SimWalker>> ws;
+            for(int l = 0; l < 64; ++l)
+            {
+                const float fx = px0 + (l >> 3) + rnd(), fy = py + rnd();
+                float ux = fx / cfg.width * 2.0f - 1.0f, uy = fy / cfg.height * 2.0f - 1.0f;
+                ux *= cam.aspect_ratio;
+                uy = -uy;
+                f3 d = normalize(v3(ux * cam.inv_focal_length, uy * cam.inv_focal_length, -1.0f));
+                wq[l] = Query{cam.position, mul_m3v3(cam.orientation, d), 0.0f, 1e9f, sf, false};
+            }
+            for(int l = 0; l < 64; ++l) ws.emplace_back(new SimWalker(v, pk, wq[l], wst[l], S, g_spec));
+            std::vector<char> act(64, 1);
+            for(;;)
+            {
+                bool any = false;
+                for(int l = 0; l < 64; ++l) any = any || act[l];
+                if(!any) break;
+                iters++;
+                for(int u = 0; u < 2; ++u)
+                {
+                    std::set<uint64_t> stepped;
+                    for(int l = 0; l < 64; ++l)
+                    {
+                        if(!act[l] || ws[l]->at_leaf()) continue;
+                        g_last_block = ~0ull;
+                        if(ws[l]->node_step()) act[l] = 0;
+                        if(g_last_block != ~0ull) stepped.insert(g_last_block);
+                    }
+                    if(!stepped.empty())
+                    {
+                        phases++;
+                        distinct += double(stepped.size());
+                        if(stepped.size() == 1) uniform++;
+                    }
+                }
+                for(int l = 0; l < 64; ++l)
+                    if(act[l] && ws[l]->wants_leaf() && ws[l]->leaf_step()) act[l] = 0;
+            }
+        }
+        printf("lockstep camera-ray waves: %.1f iterations, %.1f node phases with steps, %.1f%% on one block, %.1f blocks per phase\n",
+               iters / 200, phases / 200, 100 * uniform / phases, distinct / phases);
+        return 0;
+    }
 
     // the query mix
     std::vector<Query> qs;
