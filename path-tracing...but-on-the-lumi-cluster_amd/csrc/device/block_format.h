@@ -38,21 +38,22 @@
 // them, and each box is stored as (near planes, far planes) for that
 // octant's direction signs, so with finite reciprocals the slab test needs no
 // per-axis min/max (t of the near plane is the reference's fmin(t0, t1) of
-// that axis, the far plane's its fmax).  A walk step loads one copy (128 B,
-// eight 16-byte loads with no dependency between them), tests all four
+// that axis, the far plane's its fmax).  A walk step loads one copy (112 B
+// used of 128, seven 16-byte loads with no dependency between them), tests all four
 // boxes, continues with the first passing entry and pushes the others, each
 // with its `near`, onto a per-lane stack in reverse order; a popped entry is
 // re-checked with `near < tmax` (fact 2).  Leaves are thus met in the
 // reference's order with the reference's tmax: identical hits, ties and
 // back-face flags.
 //
-//   BlockEntry (32 B)   near.xyz | a   far.xyz | b
+//   BlockCopy (128 B: seven 16-byte rows used)
+//     rows 0-3   entry j: near.xyz | a
+//     rows 4-6   the four entries' far.xyz, packed (f[3j .. 3j+2])
 //     a: kBeLeaf | payload   leaf (BLAS: triangle index in the mesh,
 //                            TLAS: instance index), payload < 2^28
 //        kBeNone             unused slot (NaN box, never passes)
 //        otherwise           block index of the child's own block
-//     b: unused (0)
-//   octant o's copy of block k: entries [(k * 8 + o) * 4, +4)
+//   octant o's copy of block k: blocks[k * 8 + o]
 // A BVH's handle is its root block's index; the root's own box is never
 // tested (fact 1).  The records are ~113 MB for the BLASes the animation
 // uses, against 8 x 581k x 64 B = 298 MB of per-octant paired node records.
@@ -62,20 +63,22 @@
 namespace ptg {
 
 constexpr uint32_t kBlockWidth = 4;
-constexpr uint32_t kBlockEntries = 8 * kBlockWidth;   // a block: one copy per octant
+constexpr uint32_t kBlockCopies = 8;   // a block: one copy per octant
 
-struct alignas(16) BlockEntry {
-    float lo_x, lo_y, lo_z;
-    uint32_t a;
-    float hi_x, hi_y, hi_z;
-    uint32_t b;
+struct alignas(16) BlockCopy {
+    struct Near {
+        float x, y, z;
+        uint32_t a;
+    } n[kBlockWidth];                  // rows 0-3
+    float f[3 * kBlockWidth];          // rows 4-6: entry j's far planes at f[3j .. 3j+2]
+    uint32_t pad[4];                   // row 7 (keeps copies on 128-byte lines)
 };
-static_assert(sizeof(BlockEntry) == 32, "BlockEntry is two 16-byte loads");
+static_assert(sizeof(BlockCopy) == 128, "BlockCopy is one 128-byte line");
 
 constexpr uint32_t kBeLeaf = 0x80000000u;
 constexpr uint32_t kBeNone = 0x40000000u;
 constexpr uint32_t kBeIndex = 0x0FFFFFFFu;   // 28-bit block indices and payloads
-// The walker's stack words are entry `a` words (a block index, or kBeLeaf |
+// The walker's stack words are entry words (a block index, or kBeLeaf |
 // payload); a leaf word sits on top of its `near` (float bits).  kBePop
 // (a leaf word no payload can produce) means "take the next stack entry".
 constexpr uint32_t kBePop = 0xFFFFFFFFu;

@@ -3,8 +3,8 @@
 //
 // The reference arrays are repacked once into records a walk step reads
 // with independent 16-byte loads:
-//   BlockEntry 32 B  4-wide BVH blocks of both levels (block_format.h): one
-//                    128 B block per step, one layout for all eight octants.
+//   BlockCopy 128 B  4-wide BVH blocks of both levels (block_format.h), one
+//                    copy per octant: one 112-byte read per step.
 //   TriRec    48 B  the three vertex positions of triangle t of a mesh,
 //                   tris[index_offset/3 + t] (ray_query.hh:228-234 gathers
 //                   indices then positions: two dependent loads -> one).
@@ -61,7 +61,7 @@ static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
 
 // Everything a hot-path kernel reads, passed by value as a kernel argument.
 struct DevScene {
-    const BlockEntry* blocks;      // block BVH records of both levels (block_format.h), 4 entries per block
+    const BlockCopy* blocks;       // block BVH records of both levels (block_format.h), 8 copies per block
     const uint32_t* tlas_root;     // per subframe: its TLAS's root block
     const TriRec* tris;
     const InstTrav* inst_trav;

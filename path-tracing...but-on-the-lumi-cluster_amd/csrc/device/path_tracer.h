@@ -560,21 +560,21 @@ struct BlockWalker {
 
     // this octant's copy of block cur: its four entries in the order the ray
     // meets them, each box as (near planes, far planes) for the octant's
-    // signs; eight 16-byte rows
+    // signs; seven 16-byte rows
     PTG_D const v4f* block_rows(const DevScene& sc) const
     {
-        return reinterpret_cast<const v4f*>(sc.blocks + (size_t(cur) * 8u + oct) * kBlockWidth);
+        return reinterpret_cast<const v4f*>(sc.blocks + size_t(cur) * kBlockCopies + oct);
     }
 
-    // Node phase, second half: the block step on its eight rows.
+    // Node phase, second half: the block step on its seven rows.
     template<bool COUNT>
-    PTG_D int node_block(const DevScene& sc, Counters& cnt, v4f q0, v4f q1, v4f q2, v4f q3, v4f q4, v4f q5, v4f q6,
-                         v4f q7)
+    PTG_D int node_block(const DevScene& sc, Counters& cnt, v4f q0, v4f q1, v4f q2, v4f q3, v4f q4, v4f q5, v4f q6)
     {
-        const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q1.x, q1.y, q1.z, q1.w);
-        const float4 l1 = make_float4(q2.x, q2.y, q2.z, q2.w), h1 = make_float4(q3.x, q3.y, q3.z, q3.w);
-        const float4 l2 = make_float4(q4.x, q4.y, q4.z, q4.w), h2 = make_float4(q5.x, q5.y, q5.z, q5.w);
-        const float4 l3 = make_float4(q6.x, q6.y, q6.z, q6.w), h3 = make_float4(q7.x, q7.y, q7.z, q7.w);
+        // rows 0-3: entry j's near planes and word; rows 4-6: the far planes, packed
+        const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q4.x, q4.y, q4.z, 0.0f);
+        const float4 l1 = make_float4(q1.x, q1.y, q1.z, q1.w), h1 = make_float4(q4.w, q5.x, q5.y, 0.0f);
+        const float4 l2 = make_float4(q2.x, q2.y, q2.z, q2.w), h2 = make_float4(q5.z, q5.w, q6.x, 0.0f);
+        const float4 l3 = make_float4(q3.x, q3.y, q3.z, q3.w), h3 = make_float4(q6.y, q6.z, q6.w, 0.0f);
         if(COUNT) cnt.step_loads |= 1u;
         const uint32_t a0 = __float_as_uint(l0.w), a1 = __float_as_uint(l1.w), a2 = __float_as_uint(l2.w),
                        a3 = __float_as_uint(l3.w);
@@ -626,7 +626,7 @@ struct BlockWalker {
         if(const int r = node_pop(); r >= 0) return r;
         PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
         const v4f* p = block_rows(sc);
-        return node_block<COUNT>(sc, cnt, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+        return node_block<COUNT>(sc, cnt, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
     }
 
     // Leaf phase, first half: the parked triangle, else the BLAS entry or
@@ -700,7 +700,7 @@ struct BlockWalker {
 
     // PTG_WALK_SCHED 1: one step of either kind - the lane's leaf work if it
     // has any, else a node step - with both kinds' rows read by the same
-    // eight loads (a leaf lane's last four rows are unused; the record
+    // seven loads (a leaf lane's last three rows are unused; the record
     // buffers carry the slack), so a wave with lanes of both kinds waits for
     // memory once.  Returns as node_step / leaf_step.
     template<bool ANY, bool COUNT>
@@ -729,14 +729,14 @@ struct BlockWalker {
                 p = block_rows(sc);
             }
         }
-        v4f q0 = {0, 0, 0, 0}, q1 = q0, q2 = q0, q3 = q0, q4 = q0, q5 = q0, q6 = q0, q7 = q0;
+        v4f q0 = {0, 0, 0, 0}, q1 = q0, q2 = q0, q3 = q0, q4 = q0, q5 = q0, q6 = q0;
         if(load)
         {
-            q0 = p[0]; q1 = p[1]; q2 = p[2]; q3 = p[3]; q4 = p[4]; q5 = p[5]; q6 = p[6]; q7 = p[7];
+            q0 = p[0]; q1 = p[1]; q2 = p[2]; q3 = p[3]; q4 = p[4]; q5 = p[5]; q6 = p[6];
         }
         if(lf) return leaf_finish<ANY, COUNT>(sc, cnt, ls, q0, q1, q2, q3);
         if(nr >= 0) return nr;
-        return node_block<COUNT>(sc, cnt, q0, q1, q2, q3, q4, q5, q6, q7);
+        return node_block<COUNT>(sc, cnt, q0, q1, q2, q3, q4, q5, q6);
     }
 
     // One step of either phase (the per-lane walks: the megakernel and the

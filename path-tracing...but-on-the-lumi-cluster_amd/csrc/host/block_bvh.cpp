@@ -131,20 +131,10 @@ void split_wide(Tree& t)
     }
 }
 
-BlockEntry none_entry()
-{
-    const float q = std::numeric_limits<float>::quiet_NaN();
-    BlockEntry e;
-    e.lo_x = e.lo_y = e.lo_z = e.hi_x = e.hi_y = e.hi_z = q;
-    e.a = kBeNone;
-    e.b = 0;
-    return e;
-}
-
 } // namespace
 
 bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t block_base,
-                    uint32_t payload_limit, std::vector<BlockEntry>& out, BlockBvh& info, std::string& err)
+                    uint32_t payload_limit, std::vector<BlockCopy>& out, BlockBvh& info, std::string& err)
 {
     if(count == 0) { err = "empty BVH"; return false; }
     Tree t;
@@ -195,19 +185,19 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
         blks.push_back(make(0));
     for(size_t q = 0; q < blks.size(); ++q)            // breadth-first
     {
-        block_of[blks[q].root] = block_base + uint32_t(out.size() / kBlockEntries + q);
+        block_of[blks[q].root] = block_base + uint32_t(out.size() / kBlockCopies + q);
         for(uint32_t c: std::vector<uint32_t>(blks[q].slots))
             if(!t.leaf(c)) blks.push_back(make(c));
     }
-    if(uint64_t(block_base) + out.size() / kBlockEntries + blks.size() > kBeIndex)
+    if(uint64_t(block_base) + out.size() / kBlockCopies + blks.size() > kBeIndex)
     { err = "BVH records above 2^28 blocks"; return false; }
-    if(out.size() % kBlockEntries) { err = "unaligned block output"; return false; }
+    if(out.size() % kBlockCopies) { err = "unaligned block output"; return false; }
 
     // stack bound: a block step walks one passing entry and pushes the
     // others (at most all but one); a walk holds at most one block's pushes
     // per level of its path
     std::vector<uint32_t> bound(blks.size(), 0);
-    const uint32_t first = uint32_t(out.size() / kBlockEntries) + block_base;
+    const uint32_t first = uint32_t(out.size() / kBlockCopies) + block_base;
     for(size_t q = blks.size(); q-- > 0;)
     {
         uint32_t own = uint32_t(blks[q].slots.size()) - 1u, below = 0;
@@ -240,24 +230,30 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
             };
             if(t.leaf(b.root)) seq.push_back(b.root);
             else walk(walk, b.root);
-            if(seq.size() != b.slots.size()) { err = "block order lost an entry"; return false; }
+            if(seq.size() != b.slots.size() || seq.size() > W) { err = "block order lost an entry"; return false; }
+            BlockCopy bc{};
             for(uint32_t j = 0; j < W; ++j)
             {
-                if(j >= seq.size()) { out.push_back(none_entry()); continue; }
+                if(j >= seq.size())
+                {   // an unused slot: a NaN box never passes
+                    const float q = std::numeric_limits<float>::quiet_NaN();
+                    bc.n[j] = BlockCopy::Near{q, q, q, kBeNone};
+                    bc.f[3 * j] = bc.f[3 * j + 1] = bc.f[3 * j + 2] = q;
+                    continue;
+                }
                 const uint32_t c = seq[j];
                 const ptg_bvh_node& n = t.box[c];
                 const bool px = o & 1u, py = o & 2u, pz = o & 4u;
-                BlockEntry e;
-                e.lo_x = px ? n.min_x : n.max_x; e.hi_x = px ? n.max_x : n.min_x;
-                e.lo_y = py ? n.min_y : n.max_y; e.hi_y = py ? n.max_y : n.min_y;
-                e.lo_z = pz ? n.min_z : n.max_z; e.hi_z = pz ? n.max_z : n.min_z;
-                e.a = t.leaf(c) ? t.payload[c] : block_of[c];
-                e.b = 0;
-                out.push_back(e);
+                bc.n[j] = BlockCopy::Near{px ? n.min_x : n.max_x, py ? n.min_y : n.max_y, pz ? n.min_z : n.max_z,
+                                          t.leaf(c) ? t.payload[c] : block_of[c]};
+                bc.f[3 * j] = px ? n.max_x : n.min_x;
+                bc.f[3 * j + 1] = py ? n.max_y : n.min_y;
+                bc.f[3 * j + 2] = pz ? n.max_z : n.min_z;
             }
+            out.push_back(bc);
         }
     }
-    info.root = block_base + uint32_t((out.size() / kBlockEntries) - blks.size());
+    info.root = block_base + uint32_t((out.size() / kBlockCopies) - blks.size());
     info.blocks = uint32_t(blks.size());
     info.stack_entries = bound.empty() ? 0 : bound[0];
     info.max_payload = 0;
@@ -277,17 +273,18 @@ namespace ptg {
 // but the TLAS records shrink from ~51 MB to 1-2 MB and stay in L2.
 static void dedup_tlas(FramePack& fp)
 {
-    const size_t E = kBlockEntries, nb = fp.tlas.size() / E;
+    const size_t E = kBlockCopies, nb = fp.tlas.size() / E;
     if(nb == 0) return;
     std::vector<uint32_t> canon(nb);
-    std::vector<BlockEntry> uniq;   // distinct blocks, inner links as distinct-block ids
+    std::vector<BlockCopy> uniq;   // distinct blocks, inner links as distinct-block ids
     std::unordered_map<uint64_t, std::vector<uint32_t>> table;
-    BlockEntry tmp[kBlockEntries];
+    BlockCopy tmp[kBlockCopies];
     for(size_t k = nb; k-- > 0;)
     {   // BFS within each TLAS: a block's children come after it
         memcpy(tmp, &fp.tlas[k * E], sizeof(tmp));
-        for(BlockEntry& e: tmp)
-            if(!(e.a & (kBeLeaf | kBeNone))) e.a = canon[e.a - fp.tlas_base];
+        for(BlockCopy& c: tmp)
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a = canon[e.a - fp.tlas_base];
         uint64_t h = 1469598103934665603ull;   // FNV-style mix over the block's 64-bit words
         static_assert(sizeof(tmp) % 8 == 0, "whole words");
         for(size_t i = 0; i < sizeof(tmp); i += 8)
@@ -316,13 +313,14 @@ static void dedup_tlas(FramePack& fp)
     uint32_t next = 0;
     for(size_t k = 0; k < nb; ++k)
         if(pos[canon[k]] == 0xFFFFFFFFu) pos[canon[k]] = next++;
-    std::vector<BlockEntry> out(size_t(nu) * E);
+    std::vector<BlockCopy> out(size_t(nu) * E);
     for(uint32_t id = 0; id < nu; ++id)
         for(size_t j = 0; j < E; ++j)
         {
-            BlockEntry e = uniq[size_t(id) * E + j];
-            if(!(e.a & (kBeLeaf | kBeNone))) e.a = fp.tlas_base + pos[e.a];
-            out[size_t(pos[id]) * E + j] = e;
+            BlockCopy c = uniq[size_t(id) * E + j];
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a = fp.tlas_base + pos[e.a];
+            out[size_t(pos[id]) * E + j] = c;
         }
     for(uint32_t& r: fp.tlas_root) r = fp.tlas_base + pos[canon[r - fp.tlas_base]];
     fp.tlas.swap(out);
@@ -335,7 +333,7 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
                            std::string& err) const
 {
     fp = FramePack();
-    fp.blas_base = uint32_t(blas.size() / kBlockEntries);
+    fp.blas_base = uint32_t(blas.size() / kBlockCopies);
     fp.blas_stack = blas_stack;
     fp.inst_root.resize(instance_count);
     std::string why;
@@ -373,7 +371,7 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
         }
         fp.inst_root[i] = rec.root;
     }
-    fp.tlas_base = fp.blas_base + uint32_t(fp.new_blas.size() / kBlockEntries);
+    fp.tlas_base = fp.blas_base + uint32_t(fp.new_blas.size() / kBlockCopies);
     fp.tlas_root.resize(subframe_count);
     for(size_t i = 0; i < subframe_count; ++i)
     {
@@ -384,7 +382,7 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
     }
     // The subframes' TLASes are independent: packed on several host threads,
     // each at block base 0, then laid out one after another and relocated.
-    std::vector<std::vector<BlockEntry>> part(subframe_count);
+    std::vector<std::vector<BlockCopy>> part(subframe_count);
     std::vector<BlockBvh> pinfo(subframe_count);
     std::vector<std::string> perr(subframe_count);
     std::vector<char> pok(subframe_count, 0);
@@ -417,12 +415,13 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
     fp.tlas.reserve(total_entries);
     for(size_t i = 0; i < subframe_count; ++i)
     {
-        const uint32_t base = fp.tlas_base + uint32_t(fp.tlas.size() / kBlockEntries);
-        if(uint64_t(base) + part[i].size() / kBlockEntries > kBeIndex) { err = "TLAS records above 2^28 blocks"; return PTG_E_RANGE; }
-        for(BlockEntry e: part[i])
+        const uint32_t base = fp.tlas_base + uint32_t(fp.tlas.size() / kBlockCopies);
+        if(uint64_t(base) + part[i].size() / kBlockCopies > kBeIndex) { err = "TLAS records above 2^28 blocks"; return PTG_E_RANGE; }
+        for(BlockCopy c: part[i])
         {
-            if(!(e.a & (kBeLeaf | kBeNone))) e.a += base;
-            fp.tlas.push_back(e);
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a += base;
+            fp.tlas.push_back(c);
         }
         fp.tlas_root[i] = pinfo[i].root + base;
         fp.tlas_stack = std::max(fp.tlas_stack, pinfo[i].stack_entries);
@@ -431,9 +430,10 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
     // every block index a walk can follow lies inside the buffer (the
     // committed BLAS blocks were checked when they were added)
     const uint32_t total = fp.total_blocks();
-    for(const std::vector<BlockEntry>* v: {&fp.new_blas, &fp.tlas})
-        for(const BlockEntry& e: *v)
-            if(!(e.a & (kBeLeaf | kBeNone)) && e.a >= total) { err = "block link outside the block buffer"; return PTG_E_RANGE; }
+    for(const std::vector<BlockCopy>* v: {&fp.new_blas, &fp.tlas})
+        for(const BlockCopy& c: *v)
+            for(const BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone)) && e.a >= total) { err = "block link outside the block buffer"; return PTG_E_RANGE; }
     for(uint32_t r: fp.tlas_root)
         if(r >= total) { err = "TLAS root outside the block buffer"; return PTG_E_RANGE; }
     for(uint32_t r: fp.inst_root)

@@ -16,15 +16,15 @@ struct BlockBvh {
 
 // Packs one BVH given in the reference layout - nodes[0..count) and the eight
 // link orders links[o * count + i] (bvh.cc:195-229) - appending its blocks
-// (kBlockEntries entries each: kBlockWidth per octant) to `out`.  Child block
-// indices are block_base + position in `out` / kBlockEntries.  Checked, with an error in `err`:
+// (kBlockCopies copies each, one per octant) to `out`.  Child block
+// indices are block_base + position in `out` / kBlockCopies.  Checked, with an error in `err`:
 //   - the links are the reference builder's: a tree rooted at node 0 whose
 //     every order lists each node's children forward, or reversed when the
 //     octant's sign on the node's axis is not positive (bvh.cc:173-191);
 //   - every box contains its children's boxes (the walk skips inner boxes);
 //   - leaf payloads are below payload_limit (and 2^28).
 bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t block_base,
-                    uint32_t payload_limit, std::vector<BlockEntry>& out, BlockBvh& info, std::string& err);
+                    uint32_t payload_limit, std::vector<BlockCopy>& out, BlockBvh& info, std::string& err);
 
 } // namespace ptg
 
@@ -43,13 +43,13 @@ struct BlasRecord {
 struct FramePack {
     uint32_t blas_base = 0;                 // block index of new_blas[0]
     uint32_t tlas_base = 0;                 // block index of tlas[0]
-    std::vector<BlockEntry> new_blas;       // BLASes no earlier frame packed
-    std::vector<BlockEntry> tlas;           // this frame's TLASes, one per subframe
+    std::vector<BlockCopy> new_blas;       // BLASes no earlier frame packed
+    std::vector<BlockCopy> tlas;           // this frame's TLASes, one per subframe
     std::unordered_map<uint32_t, BlasRecord> new_records;
     std::vector<uint32_t> tlas_root;        // per subframe
     std::vector<uint32_t> inst_root;        // per instance: its BLAS's root block
     uint32_t blas_stack = 0, tlas_stack = 0;
-    uint32_t total_blocks() const { return tlas_base + uint32_t(tlas.size() / kBlockEntries); }
+    uint32_t total_blocks() const { return tlas_base + uint32_t(tlas.size() / kBlockCopies); }
     uint32_t stack_bound() const { return blas_stack + tlas_stack; }   // stack entries a walk can hold
 };
 
@@ -57,7 +57,7 @@ struct FramePack {
 // host half of ptg_upload_frame, kept free of device code so the CPU tests
 // (tools/walk_sim.cpp) run exactly what the upload runs.
 struct BlockCache {
-    std::vector<BlockEntry> blas;                         // committed BLAS blocks
+    std::vector<BlockCopy> blas;                         // committed BLAS blocks
     std::unordered_map<uint32_t, BlasRecord> records;     // BLAS node_offset -> record
     uint32_t blas_stack = 0;                              // largest committed BLAS stack bound
 

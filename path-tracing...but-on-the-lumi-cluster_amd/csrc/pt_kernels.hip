@@ -878,7 +878,7 @@ struct ptg_context {
     DevScene scene_args(const ptg_render_config* cfg) const
     {
         DevScene s;
-        s.blocks = blocks.as<BlockEntry>();
+        s.blocks = blocks.as<BlockCopy>();
         s.tlas_root = tlas_root.as<uint32_t>();
         s.tris = tris.as<TriRec>();
         s.inst_trav = inst_trav.as<InstTrav>();
@@ -1491,9 +1491,9 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     };
     // blocks = [BLAS blocks][TLAS blocks]; growing the buffer drops the BLAS
     // blocks already there, which are then uploaded again
-    const std::vector<BlockEntry>& old_blas = ctx->cache.blas;
+    const std::vector<BlockCopy>& old_blas = ctx->cache.blas;
     const size_t blas_total = old_blas.size() + fp.new_blas.size();
-    const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockEntry);
+    const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockCopy);
     if(need > ctx->blocks.bytes)
     {
         PTG_HIP(grow(ctx->blocks, need + need / 8));
@@ -1505,14 +1505,14 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     PTG_HIP(grow(ctx->subframes, subframe_count * sizeof(ptg_subframe)));
     PTG_HIP(grow(ctx->polygon, subframe_count * kPolyStride * sizeof(float2)));
     if(!mesh_jobs.empty()) PTG_HIP(grow(ctx->jobs, mesh_jobs.size() * sizeof(MeshJob)));
-    BlockEntry* dev = ctx->blocks.as<BlockEntry>();
+    BlockCopy* dev = ctx->blocks.as<BlockCopy>();
     struct Part { const void* src; size_t n; void* dst; };
     std::vector<Part> parts;
     if(ctx->blas_on_device < old_blas.size())
-        parts.push_back({old_blas.data() + ctx->blas_on_device, (old_blas.size() - ctx->blas_on_device) * sizeof(BlockEntry),
+        parts.push_back({old_blas.data() + ctx->blas_on_device, (old_blas.size() - ctx->blas_on_device) * sizeof(BlockCopy),
                          dev + ctx->blas_on_device});
-    parts.push_back({fp.new_blas.data(), fp.new_blas.size() * sizeof(BlockEntry), dev + old_blas.size()});
-    parts.push_back({fp.tlas.data(), fp.tlas.size() * sizeof(BlockEntry), dev + blas_total});
+    parts.push_back({fp.new_blas.data(), fp.new_blas.size() * sizeof(BlockCopy), dev + old_blas.size()});
+    parts.push_back({fp.tlas.data(), fp.tlas.size() * sizeof(BlockCopy), dev + blas_total});
     parts.push_back({fp.tlas_root.data(), subframe_count * sizeof(uint32_t), ctx->tlas_root.p});
     parts.push_back({it.data(), instance_count * sizeof(InstTrav), ctx->inst_trav.p});
     parts.push_back({is.data(), instance_count * sizeof(InstShade), ctx->inst_shade.p});

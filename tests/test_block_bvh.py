@@ -39,5 +39,5 @@ def test_block_walk_matches_link_walk(walk_sim, assets_dir, frame):
     assert block_closest < 0.6 * link_closest, r.stdout
     # the subframes' TLASes share their identical subtrees (pack_frame's
     # deduplication): ~50 MB of per-subframe blocks become 1-2 MB
-    t = re.search(r"TLAS (\d+) entries \(([0-9.]+) MB\)", r.stdout)
+    t = re.search(r"TLAS (\d+) copies \(([0-9.]+) MB\)", r.stdout)
     assert t and float(t.group(2)) < 5.0, r.stdout

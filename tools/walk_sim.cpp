@@ -181,7 +181,7 @@ std::set<uint64_t>* g_visits = nullptr;   // PACKET=1: the (instance, block) pai
 uint64_t g_last_block = ~0ull;              // the (instance, block) pair the last node step stepped
 
 struct Packed {
-    std::vector<BlockEntry> E;         // the device block buffer: [BLAS blocks][TLAS blocks]
+    std::vector<BlockCopy> E;          // the device block buffer: [BLAS blocks][TLAS blocks]
     std::vector<uint32_t> inst_root;   // per instance: BLAS root block
     std::vector<uint32_t> tlas_root;   // per subframe
 };
@@ -255,28 +255,29 @@ struct SimWalker {
         if(g_visits) g_visits->insert((uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur);
         g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur;
         // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
-        const BlockEntry* e = &pk.E[(size_t(cur) * 8u + octant(dir)) * kBlockWidth];
+        const BlockCopy& bc = pk.E[size_t(cur) * kBlockCopies + octant(dir)];
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
         for(int j = int(kBlockWidth) - 1; j >= 0; --j)
         {
-            const BlockEntry& x = e[j];
+            const BlockCopy::Near& x = bc.n[j];
+            const float* xf = &bc.f[3 * j];
             if(x.a & kBeNone) continue;
             float n;
             st.visits++;
             bool pass;
             if(fin)
             {   // the device's fast form: near = max of near-plane t, far = min of far-plane t
-                const float tnx = (x.lo_x - org.x) * inv.x, tfx = (x.hi_x - org.x) * inv.x;
-                const float tny = (x.lo_y - org.y) * inv.y, tfy = (x.hi_y - org.y) * inv.y;
-                const float tnz = (x.lo_z - org.z) * inv.z, tfz = (x.hi_z - org.z) * inv.z;
+                const float tnx = (x.x - org.x) * inv.x, tfx = (xf[0] - org.x) * inv.x;
+                const float tny = (x.y - org.y) * inv.y, tfy = (xf[1] - org.y) * inv.y;
+                const float tnz = (x.z - org.z) * inv.z, tfz = (xf[2] - org.z) * inv.z;
                 n = fmaxf_(tnx, fmaxf_(tny, tnz));
                 const float f = fminf_(tfx, fminf_(tfy, tfz));
                 pass = n <= f && f > q.tmin && n < tmax;
             }
             else
-                pass = box(org, inv, q.tmin, tmax, &x.lo_x, &x.hi_x, n);
+                pass = box(org, inv, q.tmin, tmax, &x.x, xf, n);
             if(!pass) continue;
             if(cand != kBePop) push(cand, cn);
             cand = x.a;
@@ -426,9 +427,9 @@ int main(int argc, char** argv)
     pk.E.insert(pk.E.end(), fp.tlas.begin(), fp.tlas.end());
     pk.inst_root = fp.inst_root;
     pk.tlas_root = fp.tlas_root;
-    printf("frame %u: BLAS %zu + %zu new entries (%.1f MB), TLAS %zu entries (%.1f MB); stack bound %u entries (TLAS %u)\n",
-           frame, cache.blas.size(), fp.new_blas.size(), (cache.blas.size() + fp.new_blas.size()) * 32 / 1e6, fp.tlas.size(),
-           fp.tlas.size() * 32 / 1e6, fp.stack_bound(), fp.tlas_stack);
+    printf("frame %u: BLAS %zu + %zu new copies (%.1f MB), TLAS %zu copies (%.1f MB); stack bound %u entries (TLAS %u)\n",
+           frame, cache.blas.size(), fp.new_blas.size(), (cache.blas.size() + fp.new_blas.size()) * 128 / 1e6, fp.tlas.size(),
+           fp.tlas.size() * 128 / 1e6, fp.stack_bound(), fp.tlas_stack);
 
     if(getenv("PACKET"))
     {   // how much a wave of camera rays (8 pixels x 8 jittered samples, one
