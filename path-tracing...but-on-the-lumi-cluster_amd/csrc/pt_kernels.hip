@@ -236,6 +236,9 @@ constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many
 #ifndef PTG_WALK_RESIDENT
 #define PTG_WALK_RESIDENT 4 // walk blocks per CU (LDS-bound with 16-entry stack windows: 4 x 40 KB)
 #endif
+#ifndef PTG_WALK_BLOCKS_PER_CU
+#define PTG_WALK_BLOCKS_PER_CU 3   // walk grid: blocks per CU (0: all that are resident); see ptg_context_create
+#endif
 #ifndef PTG_XCD_BANDS
 #define PTG_XCD_BANDS 1024
 #endif
@@ -1316,15 +1319,25 @@ int ptg_context_create(int device, ptg_context** out)
     if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, ctx->walk_lds[1]) == hipSuccess &&
        per_cu > 0)
         ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
-    // 4 x the resident grid: each block's static share is a quarter, and the
-    // dispatcher starts the later blocks as earlier ones retire, which trims
-    // the launch tail (measured: extend -2% on frame 0, -3.5% on frame 450)
-    uint32_t oversub = 4;
+    // One wave of walk blocks, 3 per CU although the LDS holds 4: every block
+    // is resident from the start (no oversubscription), and the fourth slot's
+    // LDS and registers take the other chunk pipeline's shade and sky waves,
+    // which cannot sit beside four walk blocks (their LDS fills the CU).
+    // Measured at 1024 spp against the round-1 choice (4 x the resident grid):
+    // frame 0 464 vs 495 ms, frame 450 2827 vs 2843, frame 1400 2004 vs 2012
+    // (profiles/r02o_grid/).  PTG_WALK_OVERSUB / PTG_WALK_BLOCKS_PER_CU /
+    // PTG_WALK_GRID / PTG_SHADOW_GRID override it for experiments.
+    uint32_t oversub = 1;
     if(const char* w = getenv("PTG_WALK_OVERSUB")) oversub = uint32_t(std::max(1, atoi(w)));
     for(int k = 0; k < 2; ++k) ctx->walk_grid[k] *= oversub;
-    if(const char* w = getenv("PTG_WALK_BLOCKS_PER_CU"))   // experiments: fewer resident walk blocks
+    uint32_t walk_per_cu = PTG_WALK_BLOCKS_PER_CU;
+    if(const char* w = getenv("PTG_WALK_BLOCKS_PER_CU")) walk_per_cu = uint32_t(std::max(0, atoi(w)));
+    if(walk_per_cu)
         for(int k = 0; k < 2; ++k)
-            ctx->walk_grid[k] = std::min(ctx->walk_grid[k], uint32_t(std::max(1, atoi(w)) * prop.multiProcessorCount));
+            ctx->walk_grid[k] = std::min(ctx->walk_grid[k], walk_per_cu * uint32_t(prop.multiProcessorCount));
+    const char* gw[2] = {getenv("PTG_WALK_GRID"), getenv("PTG_SHADOW_GRID")};   // experiments: walk grid in blocks
+    for(int k = 0; k < 2; ++k)
+        if(gw[k]) ctx->walk_grid[k] = uint32_t(std::max(8, atoi(gw[k]))) / 8u * 8u;
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
