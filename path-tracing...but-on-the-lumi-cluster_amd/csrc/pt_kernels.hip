@@ -824,6 +824,7 @@ struct ptg_context {
     int pipeline = 0;
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
+    uint32_t walk_grid_r0 = 2048;          // closest-hit walk grid of round 0 (camera rays)
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
     uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (PTG_HBM_PCT)
@@ -1057,7 +1058,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const DevScene sc = ctx->scene_args(cfg);
     // walk stack spill areas: one per (chunk pipeline, walk kind), since up to
     // four walk launches run at once; stack_bound entries per walk lane
-    const size_t spill_region = size_t(std::max(ctx->walk_grid[0], ctx->walk_grid[1])) * kBlock * ctx->stack_bound;
+    const size_t spill_region = size_t(std::max({ctx->walk_grid[0], ctx->walk_grid[1], ctx->walk_grid_r0})) * kBlock * ctx->stack_bound;
     if(wf) PTG_HIP(ctx->spill.reserve(std::max<size_t>(1, 2 * nslots * spill_region) * sizeof(uint2)));
     auto walk_scene = [&](uint32_t slot, int kind) {
         DevScene w = sc;
@@ -1117,10 +1118,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 const TraceOut& tr = trs[r & 1];
                 if(int e = timed_begin(ctx, K_EXTEND, ms)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), r ? ctx->walk_grid[0] : ctx->walk_grid_r0, dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
                 else
-                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), r ? ctx->walk_grid[0] : ctx->walk_grid_r0, dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
                                        counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
@@ -1338,6 +1339,8 @@ int ptg_context_create(int device, ptg_context** out)
     const char* gw[2] = {getenv("PTG_WALK_GRID"), getenv("PTG_SHADOW_GRID")};   // experiments: walk grid in blocks
     for(int k = 0; k < 2; ++k)
         if(gw[k]) ctx->walk_grid[k] = uint32_t(std::max(8, atoi(gw[k]))) / 8u * 8u;
+    ctx->walk_grid_r0 = ctx->walk_grid[0];
+    if(const char* w = getenv("PTG_WALK_GRID_R0")) ctx->walk_grid_r0 = uint32_t(std::max(8, atoi(w))) / 8u * 8u;
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
     PTG_HIP(hipSetDevice(device));
@@ -1345,9 +1348,19 @@ int ptg_context_create(int device, ptg_context** out)
     PTG_HIP(ctx->debug.reserve(kDebugSlots * sizeof(uint32_t)));
     PTG_HIP(hipMemset(ctx->debug.p, 0, kDebugSlots * sizeof(uint32_t)));
 #endif
+    // experiments: PTG_SIDE_PRIO / PTG_MAIN_PRIO = hi | lo give the internal
+    // side (sky, shadow) / extra-slot main streams the device's greatest /
+    // least stream priority
+    auto make_stream = [](hipStream_t* st, const char* env) {
+        const char* v = getenv(env);
+        int least = 0, greatest = 0;
+        if(v && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+            return hipStreamCreateWithPriority(st, hipStreamNonBlocking, v[0] == 'h' ? greatest : least);
+        return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    };
     if(getenv("PTG_NO_OVERLAP") == nullptr)
     {
-        PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        PTG_HIP(make_stream(&ctx->side, "PTG_SIDE_PRIO"));
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
         PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
         uint32_t slots = PTG_WF_SLOTS;
@@ -1358,8 +1371,8 @@ int ptg_context_create(int device, ptg_context** out)
             for(uint32_t k = 1; k < slots; ++k)
             {
                 ptg_context::Slot& b = ctx->slot[k];
-                PTG_HIP(hipStreamCreateWithFlags(&b.main, hipStreamNonBlocking));
-                PTG_HIP(hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking));
+                PTG_HIP(make_stream(&b.main, "PTG_MAIN_PRIO"));
+                PTG_HIP(make_stream(&b.side, "PTG_SIDE_PRIO"));
                 PTG_HIP(hipEventCreateWithFlags(&b.ev_main, hipEventDisableTiming));
                 PTG_HIP(hipEventCreateWithFlags(&b.ev_side, hipEventDisableTiming));
             }
