@@ -846,6 +846,8 @@ struct ptg_context {
     struct Slot {
         hipStream_t main = nullptr, side = nullptr;
         hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_done = nullptr, ev_acc = nullptr;
+        hipStream_t shd = nullptr;     // experiments (PTG_SHADOW_STREAM): the any-hit walk on its own stream
+        hipEvent_t ev_shd = nullptr;
         DevBuf own_state, own_samples;
         DevBuf* state = nullptr;
         DevBuf* samples = nullptr;
@@ -870,8 +872,11 @@ struct ptg_context {
                 if(st) (void)hipStreamDestroy(st);
         }
         for(uint32_t k = 0; k < kMaxSlots; ++k)
-            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc})
+        {
+            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc, slot[k].ev_shd})
                 if(e) (void)hipEventDestroy(e);
+            if(slot[k].shd) (void)hipStreamDestroy(slot[k].shd);
+        }
         for(hipEvent_t e: {ev_render_start, ev_acc_end})
             if(e) (void)hipEventDestroy(e);
         if(acc_stream) (void)hipStreamDestroy(acc_stream);
@@ -1128,17 +1133,23 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 // second stream: the previous round's sky kernel, then this round's
                 // shadow walk (independent of the closest-hit walk it runs beside)
                 hipStream_t ss = overlap ? sl.side : ms;
+                const hipStream_t shs = (overlap && sl.shd) ? sl.shd : ss;   // the any-hit walk's stream
                 if(r > 0)
                 {
-                    if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
+                    if(int e = timed_begin(ctx, K_SHADOW, shs)) return e;
                     if(ctx->counting)
-                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc_sh,
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], shs, sc_sh,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
                     else
-                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss, sc_sh,
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], shs, sc_sh,
                                            cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
                     PTG_HIP(hipGetLastError());
-                    if(int e = timed_end(ctx, ss)) return e;
+                    if(int e = timed_end(ctx, shs)) return e;
+                    if(shs != ss)
+                    {
+                        PTG_HIP(hipEventRecord(sl.ev_shd, shs));
+                        PTG_HIP(hipStreamWaitEvent(ms, sl.ev_shd, 0));
+                    }
                 }
                 uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
                 // classify/shade need the shadow results, the lists the previous sky
@@ -1169,6 +1180,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 {
                     PTG_HIP(hipEventRecord(sl.ev_main, ms));
                     PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
+                    if(sl.shd) PTG_HIP(hipStreamWaitEvent(sl.shd, sl.ev_main, 0));   // next round's NEE rays
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
@@ -1378,6 +1390,11 @@ int ptg_context_create(int device, ptg_context** out)
             }
             for(uint32_t k = 0; k < slots; ++k)
             {
+                if(getenv("PTG_SHADOW_STREAM"))
+                {
+                    PTG_HIP(make_stream(&ctx->slot[k].shd, "PTG_SIDE_PRIO"));
+                    PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_shd, hipEventDisableTiming));
+                }
                 PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_done, hipEventDisableTiming));
                 PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_acc, hipEventDisableTiming));
             }
