@@ -825,6 +825,7 @@ struct ptg_context {
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
     uint32_t walk_grid_r0 = 2048;          // closest-hit walk grid of round 0 (camera rays)
+    bool sky_early = false;                // PTG_SKY_EARLY (experiments)
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
     uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (PTG_HBM_PCT)
@@ -1164,6 +1165,23 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                                    sky_list, lc);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
+                // experiments (PTG_SKY_EARLY): the sky kernel starts right after
+                // classify, beside shade (disjoint sample slots, both only read
+                // this round's state set); the next shadow walk still waits for shade
+                const bool sky_early = overlap && ctx->sky_early;
+                if(sky_early)
+                {
+                    PTG_HIP(hipEventRecord(sl.ev_main, ms));
+                    PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
+                if(int e = timed_begin(ctx, K_SKY, ss)) return e;
+                if(ctx->counting)
+                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
+                                       cnt_for(K_SHADE));
+                else
+                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
+                PTG_HIP(hipGetLastError());
+                if(int e = timed_end(ctx, ss)) return e;
+                }
                 if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
@@ -1182,6 +1200,8 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
                     if(sl.shd) PTG_HIP(hipStreamWaitEvent(sl.shd, sl.ev_main, 0));   // next round's NEE rays
                 }
+                if(!sky_early)
+                {
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
@@ -1190,6 +1210,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
+                }
             }
             if(overlap)
             {   // join before accumulate
@@ -1352,6 +1373,7 @@ int ptg_context_create(int device, ptg_context** out)
     for(int k = 0; k < 2; ++k)
         if(gw[k]) ctx->walk_grid[k] = uint32_t(std::max(8, atoi(gw[k]))) / 8u * 8u;
     ctx->walk_grid_r0 = ctx->walk_grid[0];
+    ctx->sky_early = getenv("PTG_SKY_EARLY") != nullptr;
     if(const char* w = getenv("PTG_WALK_GRID_R0")) ctx->walk_grid_r0 = uint32_t(std::max(8, atoi(w))) / 8u * 8u;
     for(int k = 0; k < 2; ++k)
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
