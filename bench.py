@@ -90,18 +90,18 @@ def algorithmic_bytes(c):
     return 32 * visits + 60 * tris + 88 * enters + 156 * shades + 160 * samples
 
 
-def extend_bytes(c):
-    """Algorithmic bytes of the closest-hit walk kernel: per box test 32 B (the
-    reference's node + link per visit; one 32 B block entry of the block
-    walker, which tests about as many boxes as the reference visits nodes:
-    DESIGN.md section 4), per triangle test 60 B (3 x u32 + 3 x 16 B in
-    reference layout), per BLAS entry 88 B, plus per ray 48 B of ray state in
-    and 32 B of hit out."""
-    visits, tris, enters, queries = int(c[1]), int(c[2]), int(c[3]), int(c[4])
-    return 32 * visits + 60 * tris + 88 * enters + 80 * queries
+def walker_bytes(w, c):
+    """Bytes the closest-hit walk's own vector-memory instructions move per
+    step, from the counting pass (ptg_last_walk_stats + work counters): a
+    node phase reads a block copy's 7 x 16 B rows per lane that steps, a leaf
+    phase 4 x 16 B rows per lane (a 48-B TriRec and the next 16 B, or a 64-B
+    InstTrav), a started ray 48 B of path state (meta, origin, direction); a
+    finished ray writes 16 B of hit record and 16 B of barycentrics."""
+    queries = int(c[4])
+    return 112 * w["node_lanes"] + 64 * w["leaf_lanes"] + 48 * w["refill_lanes"] + 32 * queries
 
 
-def hierarchy_roofline(ent, launch_s, bytes_per_launch):
+def hierarchy_roofline(ent, launch_s):
     """Time floor of one walk launch from its PMC counts and the ceilings
     measured on this GPU for the walk's own access shape (random 16-B-per-lane
     gathers, tools/ta_probe.hip -> profiles/r02_probe/ceilings.json):
@@ -122,8 +122,7 @@ def hierarchy_roofline(ent, launch_s, bytes_per_launch):
 
     Each level's time is count / rate; the largest is the floor t_min and
     names the bound.  frac = t_min / measured time (<= 1 by construction when
-    the ceilings hold).  The algorithmic bytes over t_min give the effective
-    peak those bytes could be served at."""
+    the ceilings hold), each level in its own unit."""
     try:
         with open(CEILINGS) as fh:
             ceil = json.load(fh)
@@ -148,8 +147,7 @@ def hierarchy_roofline(ent, launch_s, bytes_per_launch):
         level("salu_issue", pmc["SQ_INSTS_SALU"], 256 * clock * 1e9, "CU scalar cycles")
     bound = max(levels, key=lambda k: levels[k]["seconds"])
     t_min = levels[bound]["seconds"]
-    return {"bound": bound, "t_min_s": t_min, "peak_GBps": bytes_per_launch / t_min / 1e9, "levels": levels,
-            "ceilings_source": os.path.relpath(CEILINGS, ROOT)}
+    return {"bound": bound, "t_min_s": t_min, "levels": levels, "ceilings_source": os.path.relpath(CEILINGS, ROOT)}
 
 
 def host_topology():
@@ -182,9 +180,13 @@ def host_topology():
 
 def cpu_baseline(assets, frame, heavy_frame):
     """Reference baseline_render (main.cc:12) on this host, bounded samples:
-    one socket's worth of OpenMP threads on frame `frame` and `heavy_frame`
-    (1280x720 x 16 spp: Msamples/s is nearly SPP-invariant), and BASELINE
-    configs[0] (frame 0, 640x360 x 32 spp) on one pinned core."""
+    frame `frame` and `heavy_frame` at 1280x720 x 16 spp (Msamples/s is
+    nearly SPP-invariant) with as many OpenMP threads as this job may use
+    (the cgroup CPU quota, at most the CPUs in its affinity mask), pinned one
+    per allowed CPU; and BASELINE configs[0] (frame 0, 640x360 x 32 spp) on
+    one pinned core.  A whole socket cannot be timed under the quota, so the
+    socket figure is a range: the per-core rate of the quota-sized run and of
+    the one-core run, each times the socket's cores."""
     from oracle import Reference
     topo = host_topology()
     try:
@@ -192,38 +194,44 @@ def cpu_baseline(assets, frame, heavy_frame):
     except (KeyError, ValueError):
         socket_cores = os.cpu_count() or 1
     quota = topo.get("cgroup_cpu_quota")
-    threads = int(os.environ.get("PTG_CPU_THREADS", "0")) or socket_cores
+    allowed = sorted(os.sched_getaffinity(0))
+    threads = int(os.environ.get("PTG_CPU_THREADS", "0")) or max(1, min(len(allowed), int(quota) if quota else len(allowed)))
+    cpus = allowed[:threads]
     ref = Reference("v3", 1280, 720, 16, 4)
     if not ref.available():
         return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference",
                 "sample": "unavailable: %s not built" % ref.exe}
-    r0 = ref.baseline(assets, frame, threads=threads, timeout=900)
-    rh = ref.baseline(assets, heavy_frame, threads=threads, timeout=900) if heavy_frame is not None else None
-    cores = min(threads, int(quota)) if quota else threads    # CPU time the job may use per second
-    out = {"value": round(r0["msamples_per_s"], 4), "unit": "Msamples/s", "cores": cores, "kind": "reference",
+    r0 = ref.baseline(assets, frame, threads=threads, timeout=900, cpus=cpus, bind="true")
+    rh = ref.baseline(assets, heavy_frame, threads=threads, timeout=900, cpus=cpus, bind="true") \
+        if heavy_frame is not None else None
+    per_core = r0["msamples_per_s"] / threads
+    out = {"value": round(r0["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads, "kind": "reference",
            "sample": "frame %d, 1280x720 x 16 spp (14.7 M samples, full frame) through the reference's own "
                      "baseline_render (main.cc:12-46, OpenMP static schedule) built from /root/reference sources "
-                     "with the reference flags (-O3 -ffast-math, -march=x86-64-v3); %d OpenMP threads = one socket's "
-                     "cores, on a job limited to %s CPUs of time; render %.2f s"
-                     % (frame, threads, quota if quota else "all", r0["render_s"]),
-           "threads": threads,
+                     "with the reference flags (-O3 -ffast-math, -march=x86-64-v3); %d OpenMP threads pinned one per "
+                     "CPU (OMP_PROC_BIND=true, CPUs %d-%d of this job's %d, quota %s); render %.2f s"
+                     % (frame, threads, cpus[0], cpus[-1], len(allowed), quota if quota else "none", r0["render_s"]),
+           "per_core": round(per_core, 4),
            "host": {k: v for k, v in topo.items() if not k.startswith("_")}}
-    if quota and quota < socket_cores:
-        est = r0["msamples_per_s"] / quota * socket_cores
-        out["socket_estimate"] = {
-            "value": round(est, 3), "cores": socket_cores,
-            "basis": "the measured rate per CPU of quota x the %d cores of one socket (linear; this job may not "
-                     "use more than %s CPUs of time, so a whole socket cannot be timed here)" % (socket_cores, quota)}
     if rh:
         out["heavy_frame"] = {"frame": heavy_frame, "value": round(rh["msamples_per_s"], 4), "threads": threads,
                               "render_s": round(rh["render_s"], 3)}
     ref0 = Reference("v3", 640, 360, 32, 4)
+    one_core = None
     if ref0.available():
-        c0 = ref0.baseline(assets, 0, threads=1, timeout=600, cpus=[topo["_first_cpu"]], bind="true")
-        out["config0_one_core"] = {"value": round(c0["msamples_per_s"], 4), "unit": "Msamples/s", "cores": 1,
+        c0 = ref0.baseline(assets, 0, threads=1, timeout=600, cpus=[cpus[0]], bind="true")
+        one_core = c0["msamples_per_s"]
+        out["config0_one_core"] = {"value": round(one_core, 4), "unit": "Msamples/s", "cores": 1,
                                    "sample": "BASELINE configs[0]: frame 0, 640x360 x 32 spp (7.37 M samples), "
                                              "OMP_NUM_THREADS=1 pinned to CPU %d; render %.2f s"
-                                             % (topo["_first_cpu"], c0["render_s"])}
+                                             % (cpus[0], c0["render_s"])}
+    if socket_cores > threads:
+        lo_hi = sorted([per_core * socket_cores] + ([one_core * socket_cores] if one_core else []))
+        out["socket_estimate"] = {
+            "range": [round(lo_hi[0], 3), round(lo_hi[-1], 3)], "cores": socket_cores,
+            "basis": "per-core rate x the %d cores of one socket, from the %d-thread run (%.4f per core) and the "
+                     "one-core config-0 run (%.4f); a socket cannot be timed in this job (quota %s CPUs)"
+                     % (socket_cores, threads, per_core, one_core or float("nan"), quota)}
     return out
 
 
@@ -233,6 +241,32 @@ def spot_rects(frame, w, h):
     b = (a * 2246822519 + 374761393) & 0xFFFFFFFF
     return [(w // 2 - 1, h // 2 - 1, 2, 2), (a % (w - 2), (a >> 16) % (h - 2), 2, 2),
             (b % (w - 2), (b >> 16) % (h - 2), 2, 2)]
+
+
+def check_spots(spots_npz, cfg):
+    """'k/n': how many of this run's animation spot rectangles equal, in
+    radiance bits and BGRA bytes, the reference's own render of the same
+    rectangles (tests/golden/bench_spots.npz: the reference built from its
+    sources, baseline_render semantics, main.cc:12-46); None when the golden
+    file holds another configuration."""
+    import numpy as np
+    path = os.path.join(ROOT, "tests", "golden", "bench_spots.npz")
+    if not os.path.exists(path):
+        return None
+    g = np.load(path)
+    if (int(g["width"]), int(g["height"]), int(g["spp"]), int(g["bounces"])) != \
+            (cfg.width, cfg.height, cfg.samples_per_pixel, cfg.max_bounces):
+        return None
+    want = {(int(f),) + tuple(int(v) for v in rc): (a, b) for f, rc, a, b in
+            zip(g["frames"], g["rects"], g["acc_bits"], g["bgra"])}
+    d = np.load(spots_npz)
+    ok = n = 0
+    for f, rc, a, b in zip(d["frames"], d["rects"], d["acc_bits"], d["bgra"]):
+        key = (int(f),) + tuple(int(v) for v in rc)
+        n += 1
+        if key in want and np.array_equal(want[key][0], a) and np.array_equal(want[key][1], b):
+            ok += 1
+    return "%d/%d" % (ok, n)
 
 
 def main():
@@ -335,6 +369,10 @@ def main():
         r.upload(scene, include_static=False)        # per-frame TLAS/instances/subframes over PCIe
         render_step()
 
+    def upload_step():
+        r.upload(scene, include_static=False)        # ptg_upload_frame: block packing + H2D, then the render
+        render_step()
+
     long_steps = cfg.width * cfg.height * cfg.samples_per_pixel > 4e9
 
     def reduce_max(v):
@@ -376,11 +414,14 @@ def main():
     step_busy_ms = {k: v[0] for k, v in kb.items() if v[2]}
     step_sum_ms = {k: v[1] for k, v in kb.items() if v[2]}
     step_launches = {k: v[2] for k, v in kb.items() if v[2]}
-    # (2) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
+    # (2) SURVEY 8(d)'s definition: W.H.SPP / (upload-frame + render + gather)
+    elapsed_upload = None if args.no_frame_setup else timed(upload_step, False)[0]
+    # (3) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
     elapsed_frame = None if args.no_frame_setup else timed(frame_step, False)[0]
 
     samples_per_step = cfg.width * cfg.height * cfg.samples_per_pixel * (world if args.shard == "frames" else 1)
     value = samples_per_step * args.steps / elapsed / 1e6
+    value_upload = samples_per_step * args.steps / elapsed_upload / 1e6 if elapsed_upload else None
     value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
 
     # (3) the heavy companion frame at the same configuration
@@ -458,6 +499,7 @@ def main():
                             bgra=np.array([t.cpu().numpy() for t in spots["bgra"]]), width=cfg.width, height=cfg.height,
                             spp=cfg.samples_per_pixel, bounces=cfg.max_bounces)
         bmps = sum(1 for f in mine if os.path.exists(os.path.join(frames_dir, "frame_%04d.bmp" % f)))
+        spots_exact = check_spots(spots_out, cfg)
         anim = {"frames_per_min": round(len(picks) / anim_s * 60.0, 3),
                 "full_animation_min": round(total_frames / (len(picks) / anim_s * 60.0), 2),
                 "msamples_per_s": round(len(picks) * cfg.width * cfg.height * cfg.samples_per_pixel / anim_s / 1e6, 3),
@@ -465,9 +507,11 @@ def main():
                 "seconds": round(anim_s, 3), "bmps_written": bmps, "frames_dir": frames_dir,
                 "spots": os.path.relpath(spots_out, ROOT) if spots_out.startswith(ROOT) else spots_out,
                 "slowest_frames_ms": [[f, round(ms, 1)] for ms, f in per_frame[:5]],
+                "spots_exact": spots_exact,
                 "step": "setup_animation_frame + per-frame upload + render + BMP write (writer thread, overlapped "
-                        "with the next frame) per frame; frames dealt to ranks round-robin; spot rectangles of "
-                        "every frame checked against the oracle by tests/test_animation_spots.py"}
+                        "with the next frame) per frame; frames dealt to ranks round-robin; spots_exact: the spot "
+                        "rectangles of every frame (radiance bits and BGRA) against the reference's own render of "
+                        "them (tests/golden/bench_spots.npz, made by tests/golden/make_anim_golden.py)"}
 
     workload = "frame %d, %dx%d, %d spp, %d bounces" % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel,
                                                          cfg.max_bounces)
@@ -478,7 +522,8 @@ def main():
             if heavy is not None or anim is not None:   # back to the metric frame for the counting passes
                 scene.setup_frame(frame)
                 r.upload(scene, include_static=False)
-            # deterministic work counters of the same render (separate counting pass, untimed)
+            # deterministic work counters and walk statistics of the same render
+            # (separate counting pass, untimed)
             if long_steps:
                 print("counting pass", file=sys.stderr, flush=True)
             r.enable_counters(True)
@@ -488,14 +533,14 @@ def main():
                 r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
             r.synchronize()
             kc = r.kernel_counters()
+            ws = r.walk_stats()
             r.enable_counters(False)
             total = sum(kc[k] for k in kc)
             per_step_samples = int(total[0])
             # dominant kernel: the closest-hit BVH walk (k_wf_walk<closest>, "extend")
-            ext_bytes = extend_bytes(kc["extend"])                  # algorithmic bytes per step
+            wb = walker_bytes(ws["extend"], kc["extend"])           # bytes its own loads and stores move per step
             launches = step_launches["extend"] / args.steps
             busy_ms = step_busy_ms["extend"] / args.steps            # union of its launch intervals per step
-            achieved = ext_bytes / (busy_ms * 1e-3) / 1e9
             # the same kernel with nothing beside it: one untimed render with every
             # kernel on one stream (the timed steps run up to 4 kernels at once)
             if long_steps:
@@ -510,52 +555,78 @@ def main():
             kb_iso = r.kernel_busy()
             r.enable_timing(False)
             r.set_concurrency(args.concurrency)
-            iso_ms = kb_iso["extend"][1] / max(1, kb_iso["extend"][2])
-            iso_bytes = ext_bytes / max(1, kb_iso["extend"][2])     # one launch's algorithmic bytes
-            iso_achieved = iso_bytes / (iso_ms * 1e-3) / 1e9
+            iso_launches = max(1, kb_iso["extend"][2])
+            iso_ms = kb_iso["extend"][1] / iso_launches
             ent, prof_src = pmc_profile("extend", workload, iso_ms)
-            hier = hierarchy_roofline(ent, iso_ms * 1e-3, iso_bytes) if ent else None
+            hier = hierarchy_roofline(ent, iso_ms * 1e-3) if ent else None
             path_ms = elapsed / args.steps * 1e3
             path_bytes = algorithmic_bytes(total)
-            roof = {"bound": hier["bound"] if hier else "hbm",
-                    "achieved": round(achieved, 2),
-                    "peak": round(hier["peak_GBps"], 2) if hier else HBM_PEAK_GBS,
-                    "unit": "GB/s",
-                    "frac": round(hier["t_min_s"] * launches / (busy_ms * 1e-3), 5) if hier else
-                    round(achieved / HBM_PEAK_GBS, 5),
-                    "traffic": int(ent["derived"]["hbm_side_bytes"]) if ent else None,
-                    "traffic_source": prof_src and ("%s (rocprofv3 --pmc passes of this workload, per launch: "
-                                                    "FETCH_SIZE x 1 KiB x 2 + WRITE_SIZE x 1 KiB)" % prof_src),
-                    "kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)",
-                    "basis": "achieved = the walk's algorithmic bytes per step (SURVEY 8(d) terms from the "
-                             "counting pass) / its busy time per step (union of its launch intervals, HIP events "
-                             "on the launch streams; the two chunk pipelines' walks overlap and are counted "
-                             "once); peak = those bytes / the launch's time floor over the memory-hierarchy "
-                             "levels (see 'levels': counts from the PMC profile, ceilings measured for the "
-                             "walk's access shape); frac = floor / measured time",
-                    "ms_per_launch": round(busy_ms / launches, 4), "launches_per_step": launches,
-                    "bytes_per_launch": int(ext_bytes / launches),
-                    "kernel_busy_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_busy_ms.items()},
-                    "kernel_sum_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_sum_ms.items()},
-                    "isolated": {"ms_per_launch": round(iso_ms, 4), "achieved": round(iso_achieved, 2),
-                                 "frac": round(hier["t_min_s"] / (iso_ms * 1e-3), 5) if hier else None,
-                                 "basis": "one extra untimed render with every kernel on one stream "
-                                          "(ptg_set_concurrency(0))"},
-                    "levels": {k: {"frac_isolated": round(v["frac"], 4), "count_per_launch": v["count"],
-                                   "unit": v["unit"], "ceiling_per_s": v["ceiling_per_s"]}
-                               for k, v in hier["levels"].items()} if hier else None,
-                    "ceilings_source": hier["ceilings_source"] if hier else None,
-                    "hbm_peak_GBps": HBM_PEAK_GBS,
-                    "algorithmic_frac_of_hbm_peak": round(achieved / HBM_PEAK_GBS, 5),
-                    "hot_path": {"achieved_GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
-                                 "basis": "wall time per step",
-                                 "algorithmic_bytes_per_sample": round(path_bytes / per_step_samples, 1),
-                                 "formula": "32 visits + 60 tri + 88 enter + 156 shade + 160 per sample (SURVEY 8d)"},
-                    "per_sample": {"node_visits": round(total[1] / per_step_samples, 2),
-                                   "triangle_tests": round(total[2] / per_step_samples, 2),
-                                   "blas_entries": round(total[3] / per_step_samples, 2),
-                                   "ray_queries": round(total[4] / per_step_samples, 3),
-                                   "shades": round(total[5] / per_step_samples, 3)}}
+            w = ws["extend"]
+            lanes = {"node_phase": round(w["node_lanes"] / max(1, w["node_phases"]), 2),
+                     "leaf_phase": round(w["leaf_lanes"] / max(1, w["leaf_phases"]), 2),
+                     "refill": round(w["refill_lanes"] / max(1, w["refills"]), 2),
+                     "active_per_iteration": round(w["active_lanes"] / max(1, w["iterations"]), 2)}
+            roof = {"kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)"}
+            if hier:
+                top = hier["levels"][hier["bound"]]
+                live_s = busy_ms * 1e-3 / launches                   # one launch's share of the live busy time
+                roof.update({
+                    "bound": hier["bound"],
+                    # in the bound level's own unit: its count per launch over the
+                    # live time per launch, against that level's measured ceiling
+                    "achieved": round(top["count"] / live_s / 1e9, 3),
+                    "peak": round(top["ceiling_per_s"] / 1e9, 3),
+                    "unit": "G " + top["unit"] + " per s",
+                    "frac": round(top["count"] / live_s / top["ceiling_per_s"], 5),
+                    "traffic": int(ent["derived"]["hbm_side_bytes"]),
+                    "traffic_source": "%s (rocprofv3 --pmc passes of this workload, per launch: FETCH_SIZE x 1 KiB "
+                                      "x 2 + WRITE_SIZE x 1 KiB)" % prof_src,
+                    "basis": "bound = the memory/issue level with the largest time floor for one launch (count "
+                             "from the committed PMC profile of this workload / ceiling measured on MI355X for the "
+                             "walk's access shape, see 'levels'); achieved = that count / the launch's live time "
+                             "(busy time per step, union of its launch intervals on HIP events, / launches per "
+                             "step); frac = achieved / peak = floor / live time",
+                    "levels": {k: {"count_per_launch": v["count"], "unit": v["unit"],
+                                   "ceiling_per_s": v["ceiling_per_s"], "frac_isolated": round(v["frac"], 4),
+                                   "frac_live": round(v["seconds"] / live_s, 4)} for k, v in hier["levels"].items()},
+                    "ceilings_source": hier["ceilings_source"],
+                    "hbm": {"bytes_per_launch": int(ent["derived"]["hbm_side_bytes"]),
+                            "achieved_GBps": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9, 2),
+                            "peak_GBps": HBM_PEAK_GBS,
+                            "frac": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9 / HBM_PEAK_GBS, 5)}})
+            else:
+                roof.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                             "traffic": None,
+                             "basis": "no committed PMC profile of this workload whose launch time agrees with "
+                                      "this run's (%.3f ms): levels not derived" % iso_ms})
+            roof.update({
+                "ms_per_launch": round(busy_ms / launches, 4), "launches_per_step": launches,
+                "isolated": {"ms_per_launch": round(iso_ms, 4),
+                             "frac": round(hier["t_min_s"] / (iso_ms * 1e-3), 5) if hier else None,
+                             "basis": "one extra untimed render with every kernel on one stream "
+                                      "(ptg_set_concurrency(0))"},
+                "walker_bytes": {"per_launch": int(wb / launches),
+                                 "achieved_GBps": round(wb / (busy_ms * 1e-3) / 1e9, 2),
+                                 "basis": "bytes the walk's own vector-memory instructions move (counting pass, "
+                                          "ptg_last_walk_stats): 7 x 16 B block rows per node-phase lane, 4 x 16 B "
+                                          "record rows per leaf-phase lane, 48 B of ray state per started ray, 32 B "
+                                          "of result per finished ray; mostly served by L2 and the Infinity Cache, "
+                                          "so it is compared with no HBM figure"},
+                "lanes_per_vmem_instruction": lanes,
+                "kernel_busy_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_busy_ms.items()},
+                "kernel_sum_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_sum_ms.items()},
+                "reference_equivalent_bytes_rate": {
+                    "GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
+                    "bytes_per_sample": round(path_bytes / per_step_samples, 1),
+                    "basis": "SURVEY 8(d)'s formula, 32 visits + 60 tri + 88 enter + 156 shade + 160 per sample: "
+                             "what the REFERENCE's stackless walk would read per sample, over the wall time per "
+                             "step.  Not a memory rate of this code (the block walker reads other records, mostly "
+                             "from cache) and not comparable with HBM peak"},
+                "per_sample": {"node_visits": round(total[1] / per_step_samples, 2),
+                               "triangle_tests": round(total[2] / per_step_samples, 2),
+                               "blas_entries": round(total[3] / per_step_samples, 2),
+                               "ray_queries": round(total[4] / per_step_samples, 3),
+                               "shades": round(total[5] / per_step_samples, 3)}})
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -581,6 +652,11 @@ def main():
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
             "heavy_frame": heavy,
             "animation": anim,
+            "value_survey_def": None if value_upload is None else {
+                "value": round(value_upload, 3), "unit": "Msamples/s",
+                "ms_per_step": round(elapsed_upload / args.steps * 1e3, 3),
+                "step": "SURVEY 8(d): ptg_upload_frame (TLAS block packing + H2D of the frame's records) + render "
+                        "(+ gather), the frame's host arrays already set up"},
             "with_frame_setup": None if value_frame is None else {
                 "value": round(value_frame, 3), "unit": "Msamples/s",
                 "ms_per_step": round(elapsed_frame / args.steps * 1e3, 3),
@@ -592,7 +668,8 @@ def main():
         if cpu and cpu.get("value"):
             result["gpu_vs_cpu"] = round(value / cpu["value"], 2)
             if cpu.get("socket_estimate"):
-                result["gpu_vs_cpu_socket_estimate"] = round(value / cpu["socket_estimate"]["value"], 2)
+                lo, hi = cpu["socket_estimate"]["range"]
+                result["gpu_vs_cpu_socket_estimate"] = [round(value / hi, 2), round(value / lo, 2)]
             if heavy and cpu.get("heavy_frame"):
                 result["heavy_gpu_vs_cpu"] = round(heavy["value"] / cpu["heavy_frame"]["value"], 2)
         print(json.dumps(result), flush=True)

@@ -101,6 +101,11 @@ void ptg_render_config_default(ptg_render_config* cfg);
 int ptg_abi_version(void);
 /* Message of the last error raised on this host thread ("" if none). */
 const char* ptg_last_error(void);
+/* Host worker threads each of this process's pools (scene load, per-frame
+ * TLAS builds, TLAS block packing) may use; 0 (default) = automatic: the CPUs
+ * the process may run on (affinity, cgroup CPU quota) divided by the ranks of
+ * the node (LOCAL_WORLD_SIZE).  Returns the value now in effect. */
+int ptg_set_host_threads(int threads);
 
 /* ---- host-side scene (restatement of scene.cc / bvh.cc / mesh.cc) -------
  * Produces exactly the arrays the reference's load_scene (scene.cc:135) and
@@ -149,7 +154,9 @@ typedef struct ptg_context ptg_context;
  * PTG_E_NODEVICE if the device is not a gfx950 part. */
 int ptg_context_create(int device, ptg_context** out);
 void ptg_context_destroy(ptg_context* ctx);
-/* hipStream_t the context launches on (NULL = legacy default stream). */
+/* hipStream_t the context launches on (NULL = legacy default stream).  Work
+ * already queued on the previous stream is ordered before anything queued on
+ * the new one (an event recorded there, waited on by the new stream). */
 int ptg_context_set_stream(ptg_context* ctx, void* hip_stream);
 
 /* Once per run: the static part of the arrays (everything load_scene
@@ -228,8 +235,8 @@ int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4*
 int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* rays, uint32_t* hits);
 
 /* Work counters of the last ptg_render* call (filled only while counting is
- * on: ptg_counters_enable, or PTG_COUNTERS=1 at context creation; counting
- * uses a separate, slower build of the kernel):
+ * on, ptg_counters_enable; counting uses a separate, slower build of the
+ * kernels):
  * [0] samples, [1] node visits, [2] triangle tests, [3] BLAS entries,
  * [4] ray queries, [5] closest-hit shades, [6] TLAS node visits (part of [1]),
  * [7] walk-loop iterations of whole waves (diagnostics). */
@@ -237,6 +244,16 @@ int ptg_counters_enable(ptg_context* ctx, int enable);
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
 /* Counters split by kernel kind (same kinds as ptg_last_kernel_times). */
 int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
+/* Wavefront walk statistics of the last counted ptg_render* call, for the
+ * closest-hit walk (out[0]) and the any-hit walk (out[1]):
+ * [0] node phases that loaded block rows (wave instructions of one row),
+ * [1] lanes those phases served, [2] leaf phases that loaded a triangle or
+ * instance record, [3] lanes they served, [4] refills that started rays,
+ * [5] lanes they started, [6] walk-loop iterations, [7] lanes active in them.
+ * A node phase issues 7 row loads and a leaf phase 4, each a wave
+ * instruction whatever its EXEC mask: [1]/[0] and [3]/[2] are the lanes per
+ * vector-memory instruction of the walk. */
+int ptg_last_walk_stats(ptg_context* ctx, uint64_t out[2][8]);
 
 /* Per-launch device timing, measured with HIP events recorded around every
  * kernel launch on the context's stream.  Enabling (re)starts the record;
@@ -262,16 +279,20 @@ int ptg_last_kernel_busy(ptg_context* ctx, double busy_ms[8], double ms[8], uint
 /* Execution strategy of ptg_render*: 0 = wavefront pipeline (default:
  * camera / extend / shadow / shade kernels over compacted path queues),
  * 1 = megakernel (one work-item runs a whole path).  Both produce identical
- * bits; PTG_PIPELINE=megakernel selects 1 at context creation. */
+ * bits. */
 int ptg_set_pipeline(ptg_context* ctx, int pipeline);
 
 /* Concurrency of the wavefront pipeline: 0 = every kernel on the context's
  * stream; 1 = the sky and shadow kernels on a second stream beside the walks;
  * 2 (default) = in addition two sample chunks in flight on their own stream
- * pairs, folded in sample order.  All levels produce identical bits.  Levels
- * above what the context created (PTG_NO_OVERLAP, PTG_SLOTS) act as the
- * highest available one. */
+ * pairs, folded in sample order.  All levels produce identical bits. */
 int ptg_set_concurrency(ptg_context* ctx, int level);
+
+/* Device memory the wavefront path state may take: at most `percent` (5-70,
+ * default 35) of the GPU's HBM per chunk pipeline, and never more than 85% of
+ * what is free.  A smaller share means smaller sample chunks (more launches);
+ * the bits do not change. */
+int ptg_set_hbm_share(ptg_context* ctx, int percent);
 
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);

@@ -26,9 +26,15 @@
 //   tonemap  <in.f32> <out.bgra>                     tonemap_pixel over N x 4 floats
 //   pcg      <in.u32> <out.u32>                      N x 4 seeds -> pcg4d(seed), then
 //                                                    generate_uniform_random4 bits
+//   anim_hashes <f0> <f1> <out.txt>                  per-frame SHA-256 of instances, subframes,
+//                                                    TLAS nodes and links, frames [f0, f1)
+//   anim_render <f0> <f1> <out.txt>                  per-frame SHA-256 of the whole rendered
+//                                                    image (radiance bits, BGRA), frames [f0, f1)
+//   spots    <in.txt> <out.bin>                      baseline_render over listed rectangles
 #include "scene.hh"
 #include "path_tracer.hh"
 #include "bmp.hh"
+#include "sha256.h"
 #include <chrono>
 #include <clocale>
 #include <cstdio>
@@ -242,6 +248,158 @@ static int cmd_rays(const char* assets, int argc, char** argv)
     return 0;
 }
 
+// ---- whole-animation pins ---------------------------------------------------
+// The padding words of the reference structs are not data (never written by
+// the reference): instances keep words 0-5 and 8-39 (bvh.hh:73-79), subframes
+// the words make_golden.py's scene_hashes keeps (scene.hh:7-34).
+static const int kInstKeep[] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
+                                26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39};
+static const int kSubKeep[] = {0, 1, 4, 5, 6, 8, 9, 10, 12, 13, 14, 16, 17, 18, 20, 21, 22, 23, 24, 25,
+                               28, 29, 30, 32, 33, 34, 36};
+
+template<typename T, size_t N>
+static std::string masked_hash(const std::vector<T>& v, const int (&keep)[N])
+{
+    static_assert(sizeof(T) == 160, "160-byte records");
+    ptgref::Sha256 h;
+    for(const T& r: v)
+    {
+        uint32_t w[40], out[N];
+        memcpy(w, &r, 160);
+        for(size_t k = 0; k < N; ++k) out[k] = w[keep[k]];
+        h.update(out, sizeof(out));
+    }
+    return h.hex();
+}
+
+// anim_hashes <f0> <f1> <out.txt>: load_scene once, then for every frame
+// f in [f0, f1) setup_animation_frame(s, f) (scene.cc:271-718, which pops the
+// previous frame's TLASes itself) and one line
+//   frame instances subframes tlas_nodes static_nodes sha(inst) sha(sub) sha(tlas nodes) sha(tlas links)
+static int cmd_anim_hashes(const char* assets, int argc, char** argv)
+{
+    const uint f0 = atoi(argv[0]), f1 = atoi(argv[1]);
+    scene s = load(assets, f0);
+    const size_t stat = s.bvh_buf.nodes.size() - [&] {
+        size_t n = 0;
+        for(const subframe& sf: s.subframes) n += sf.tlas.node_count;
+        return n;
+    }();
+    FILE* f = fopen(argv[2], "w");
+    if(!f) { fprintf(stderr, "cannot write %s\n", argv[2]); return 2; }
+    char cwd[4096];
+    if(!getcwd(cwd, sizeof(cwd)) || chdir(assets) != 0) return 2;
+    for(uint fr = f0; fr < f1; ++fr)
+    {
+        if(fr != f0) setup_animation_frame(s, fr);
+        ptgref::Sha256 hn, hl;
+        hn.update(s.bvh_buf.nodes.data() + stat, (s.bvh_buf.nodes.size() - stat) * sizeof(bvh_node));
+        hl.update(s.bvh_buf.links.data() + 8 * stat, (s.bvh_buf.links.size() - 8 * stat) * sizeof(bvh_link));
+        fprintf(f, "%u %zu %zu %zu %zu %s %s %s %s\n", fr, s.instances.size(), s.subframes.size(),
+                s.bvh_buf.nodes.size() - stat, stat, masked_hash(s.instances, kInstKeep).c_str(),
+                masked_hash(s.subframes, kSubKeep).c_str(), hn.hex().c_str(), hl.hex().c_str());
+        fflush(f);
+    }
+    fclose(f);
+    if(chdir(cwd) != 0) return 2;
+    return 0;
+}
+
+// anim_render <f0> <f1> <out.txt>: every frame in [f0, f1) rendered whole with
+// baseline_render's semantics (main.cc:16-43: j-ordered float sum, /SPP,
+// tonemap_pixel); one line per frame
+//   frame sha(radiance xyz f32 bits, [H][W][3]) sha(BGRA bytes, [H][W][4])
+static int cmd_anim_render(const char* assets, int argc, char** argv)
+{
+    const uint f0 = atoi(argv[0]), f1 = atoi(argv[1]);
+    scene s = load(assets, f0);
+    FILE* f = fopen(argv[2], "w");
+    if(!f) { fprintf(stderr, "cannot write %s\n", argv[2]); return 2; }
+    char cwd[4096];
+    if(!getcwd(cwd, sizeof(cwd))) return 2;
+    const uint n = IMAGE_WIDTH * IMAGE_HEIGHT;
+    std::vector<float> rad(size_t(n) * 3);
+    std::vector<uchar4> image(n);
+    for(uint fr = f0; fr < f1; ++fr)
+    {
+        if(fr != f0)
+        {
+            if(chdir(assets) != 0) return 2;
+            setup_animation_frame(s, fr);
+            if(chdir(cwd) != 0) return 2;
+        }
+        #pragma omp parallel for schedule(dynamic, 4)
+        for(uint i = 0; i < n; ++i)
+        {
+            const uint x = i % IMAGE_WIDTH, y = i / IMAGE_WIDTH;
+            float3 c = {0, 0, 0};
+            for(uint j = 0; j < SAMPLES_PER_PIXEL; ++j) c += sample_at(s, x, y, j);
+            c /= SAMPLES_PER_PIXEL;
+            rad[size_t(i) * 3 + 0] = c.x;
+            rad[size_t(i) * 3 + 1] = c.y;
+            rad[size_t(i) * 3 + 2] = c.z;
+            image[i] = tonemap_pixel(c);
+        }
+        ptgref::Sha256 hr, hb;
+        hr.update(rad.data(), rad.size() * sizeof(float));
+        hb.update(image.data(), image.size() * sizeof(uchar4));
+        fprintf(f, "%u %s %s\n", fr, hr.hex().c_str(), hb.hex().c_str());
+        fflush(f);
+    }
+    fclose(f);
+    return 0;
+}
+
+// spots <in.txt> <out.bin>: rectangles "frame x0 y0 w h" (one per line,
+// grouped by frame) rendered with baseline_render's semantics; out: per pixel
+// (rectangles in input order, rows of each) radiance xyz f32 + BGRA (16 B).
+// The samples of a pixel are computed in parallel and summed in j order.
+static int cmd_spots(const char* assets, int argc, char** argv)
+{
+    FILE* in = fopen(argv[0], "r");
+    if(!in) { fprintf(stderr, "cannot open %s\n", argv[0]); return 2; }
+    struct Rect { uint f, x0, y0, w, h; };
+    std::vector<Rect> rects;
+    Rect r;
+    while(fscanf(in, "%u %u %u %u %u", &r.f, &r.x0, &r.y0, &r.w, &r.h) == 5) rects.push_back(r);
+    fclose(in);
+    if(rects.empty()) return 2;
+    scene s = load(assets, rects[0].f);
+    uint cur = rects[0].f;
+    char cwd[4096];
+    if(!getcwd(cwd, sizeof(cwd))) return 2;
+    std::vector<uint32_t> out;
+    std::vector<float3> samp(SAMPLES_PER_PIXEL);
+    for(const Rect& q: rects)
+    {
+        if(q.f != cur)
+        {
+            if(chdir(assets) != 0) return 2;
+            setup_animation_frame(s, q.f);
+            if(chdir(cwd) != 0) return 2;
+            cur = q.f;
+        }
+        for(uint y = q.y0; y < q.y0 + q.h; ++y)
+            for(uint x = q.x0; x < q.x0 + q.w; ++x)
+            {
+                #pragma omp parallel for schedule(dynamic, 8)
+                for(uint j = 0; j < SAMPLES_PER_PIXEL; ++j) samp[j] = sample_at(s, x, y, j);
+                float3 c = {0, 0, 0};
+                for(uint j = 0; j < SAMPLES_PER_PIXEL; ++j) c += samp[j];
+                c /= SAMPLES_PER_PIXEL;
+                const uchar4 b = tonemap_pixel(c);
+                uint32_t w[4];
+                memcpy(&w[0], &c.x, 4);
+                memcpy(&w[1], &c.y, 4);
+                memcpy(&w[2], &c.z, 4);
+                memcpy(&w[3], &b, 4);
+                out.insert(out.end(), w, w + 4);
+            }
+    }
+    write_vec(argv[1], out);
+    return 0;
+}
+
 static int cmd_tonemap(int argc, char** argv)
 {
     std::vector<char> raw = read_all(argv[0]);
@@ -284,6 +442,9 @@ int main(int argc, char** argv)
     if(cmd == "render" && n == 2) return cmd_render(assets, n, a);
     if(cmd == "baseline" && n == 2) return cmd_baseline(assets, n, a);
     if(cmd == "rays" && n == 4) return cmd_rays(assets, n, a);
+    if(cmd == "anim_hashes" && n == 3) return cmd_anim_hashes(assets, n, a);
+    if(cmd == "anim_render" && n == 3) return cmd_anim_render(assets, n, a);
+    if(cmd == "spots" && n == 2) return cmd_spots(assets, n, a);
     if(cmd == "tonemap" && n == 2) return cmd_tonemap(n, a);
     if(cmd == "pcg" && n == 2) return cmd_pcg(n, a);
     fprintf(stderr, "bad command %s\n", cmd.c_str());

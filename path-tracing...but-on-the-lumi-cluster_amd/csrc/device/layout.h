@@ -21,23 +21,6 @@
 
 namespace ptg {
 
-// Non-temporal (streaming) accesses for data that passes through once per
-// round - path state, trace results, per-sample results - so that it does not
-// evict BVH records from L2 and the Infinity Cache.  1: the walks' accesses;
-// 2: every kernel's path state; 3 (default): also the per-sample results.
-// Measured at 1024 spp: frame 0 -1.3%, frame 450 -1.1% (levels 2 and 3 alike).
-#ifndef PTG_NT_STATE
-#define PTG_NT_STATE 3
-#endif
-#ifndef PTG_MISS_BARY
-#define PTG_MISS_BARY 1     // sky kernel: no hit / barycentric reads, walk: no barycentric write for a miss
-#endif
-#ifndef PTG_CLASSIFY_FLAG
-#define PTG_CLASSIFY_FLAG 1 // k_wf_classify takes "NEE pending and unoccluded" from the shadow flags alone
-#endif
-#ifndef PTG_NEE_LAZY
-#define PTG_NEE_LAZY 2      // shade/sky read (1) and write (2) a path's NEE records only when it has a pending NEE ray
-#endif
 struct alignas(16) TriRec {
     float p0x, p0y, p0z, p1x;
     float p1y, p1z, p2x, p2y;

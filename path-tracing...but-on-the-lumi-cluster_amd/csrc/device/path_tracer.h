@@ -23,16 +23,9 @@ constexpr float EARTH_RADIUS = 6.3781e6f;
 constexpr float ATMOSPHERE_HEIGHT = 1.0e5f;
 constexpr float RAYLEIGH_SCALE_HEIGHT = 7994.0f;
 constexpr float MIE_SCALE_HEIGHT = 1200.0f;
-#ifndef PTG_FAST_DIV
-#define PTG_FAST_DIV 1   // -height / scale height via div_by (== the IEEE division for every float, ref_math.h)
-#endif
-#if PTG_FAST_DIV
+// -height / scale height via div_by (== the IEEE division for every float, ref_math.h)
 PTG_D float ray_h(float h) { return div_by(-h, RAYLEIGH_SCALE_HEIGHT, 1.0f / RAYLEIGH_SCALE_HEIGHT); }
 PTG_D float mie_h(float h) { return div_by(-h, MIE_SCALE_HEIGHT, 1.0f / MIE_SCALE_HEIGHT); }
-#else
-PTG_D float ray_h(float h) { return -h / RAYLEIGH_SCALE_HEIGHT; }
-PTG_D float mie_h(float h) { return -h / MIE_SCALE_HEIGHT; }
-#endif
 constexpr float MIE_ANISOTROPY = 0.80f;
 constexpr float MIN_RAY_DIST = 1e-4f;
 constexpr float MAX_RAY_DIST = 1e9f;
@@ -56,7 +49,7 @@ constexpr int SECONDARY_ITERATIONS = 4;
 
 struct Counters {
     uint32_t visits = 0, tri_tests = 0, blas_entries = 0, queries = 0, shades = 0, tlas_visits = 0, iters = 0;
-    uint32_t step_loads = 0;   // PTG_VMEM_STATS: loads of the last step (1 record, 2 triangle, 4 instance)
+    uint32_t step_loads = 0;   // walk statistics: loads of the last step (1 block rows, 2 triangle, 4 instance)
 };
 
 struct Hit {
@@ -65,20 +58,8 @@ struct Hit {
     bool back_face;
 };
 
-#ifndef PTG_PEND
-#define PTG_PEND 1   // park a reached triangle and keep walking (BlockWalker::park)
-#endif
-#ifndef PTG_PK_SLAB
-#define PTG_PK_SLAB 0
-#endif
-#ifndef PTG_FAST_RCP
-#define PTG_FAST_RCP 1   // the walk's reciprocals via rcp_rn (== 1.0f / x for every x, ref_math.h)
-#endif
-#if PTG_FAST_RCP
+// the walk's reciprocals via rcp_rn (== 1.0f / x for every x, ref_math.h)
 PTG_D float wrcp(float x) { return rcp_rn(x); }
-#else
-PTG_D float wrcp(float x) { return 1.0f / x; }
-#endif
 PTG_D float rcp_or_big(float d) { return d == 0 ? __builtin_inff() : wrcp(d); }   // 1/d, 0 -> (float)1e40
 PTG_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 PTG_D uint32_t octant(f3 d) { return (d.x > 0 ? 1u : 0u) | (d.y > 0 ? 2u : 0u) | (d.z > 0 ? 4u : 0u); }
@@ -223,45 +204,6 @@ struct LdsCold {
     }
 };
 
-// World ray and best hit all in registers, the best hit kept as LdsCold
-// keeps it (4 registers: thit is the walk's tmax).
-struct LeanCold {
-    f3 o, d;
-    float bu, bv;
-    uint32_t binst, bprim;     // bprim: primitive | back_face << 31
-
-    PTG_D void init(f3 ro, f3 rd, f3)
-    {
-        o = ro;
-        d = rd;
-        bu = bv = 0.0f;
-        binst = 0xFFFFFFFFu;
-        bprim = 0;
-    }
-    PTG_D f3 world_o() const { return o; }
-    PTG_D f3 world_d() const { return d; }
-    PTG_D void confirm(float u, float v, float, uint32_t instance, uint32_t prim, bool back)
-    {
-        bu = u;
-        bv = v;
-        binst = instance;
-        bprim = prim | (back ? 0x80000000u : 0u);
-    }
-    PTG_D Hit result(float tmax) const
-    {
-        const bool hit = binst != 0xFFFFFFFFu;
-        Hit h;
-        h.bx = bu;
-        h.by = bv;
-        h.bz = hit ? 1.0f - bu - bv : 0.0f;
-        h.thit = hit ? tmax : -1.0f;
-        h.instance_id = binst;
-        h.primitive_id = bprim & 0x7FFFFFFFu;
-        h.back_face = (bprim >> 31) != 0;
-        return h;
-    }
-};
-
 // Per-lane walk stacks of (word, near) entries (block_format.h: word = a
 // block index or kBeLeaf | payload; near = the entry distance, re-checked
 // against tmax when the entry is popped).
@@ -288,11 +230,8 @@ struct PrivStack {
 // those entries come back one by one when the stack unwinds to them.  A
 // 16-entry window holds the whole stack for all but ~0.03 entries per query
 // of a heavy frame.
-#ifndef PTG_LDS_STACK
-#define PTG_LDS_STACK 16
-#endif
 struct LdsStack {
-    static constexpr uint32_t kCap = PTG_LDS_STACK;
+    static constexpr uint32_t kCap = 16;
     lds_uint2_t* s;            // the lane's window column: slot k at s[64 * k]
     lds_uint2_t* t;            // next free slot: s + 64 * (sp - lo)
     uint2* g;                  // the lane's spill area (HBM)
@@ -375,7 +314,7 @@ struct BlockWalker {
     uint32_t tri_base, inst, bsp;
     uint32_t cur;              // next block, leaf word, or kBePop
     float cnear;               // cur's entry distance (a leaf's is re-checked when it is tested)
-    uint32_t pend;             // PTG_PEND: a parked triangle (leaf word), or kBePop
+    uint32_t pend;             // a parked triangle (leaf word), or kBePop
     float pnear;               // its entry distance
 
     // ray_query_initialize (ray_query.hh:111-151); root = the TLAS's root
@@ -404,22 +343,12 @@ struct BlockWalker {
     }
     PTG_D Hit result() const { return cold.result(tmax); }
 
-    // slab test (ray_query.hh:197-207) with its entry distance.  PTG_PK_SLAB:
-    // the subtractions and products as packed pairs (lo, hi) per axis -
-    // v_pk_add_f32 / v_pk_mul_f32 round each lane exactly as the scalar ops
-    typedef float v2f __attribute__((ext_vector_type(2)));
+    // slab test (ray_query.hh:197-207) with its entry distance
     PTG_D bool box(float4 lo, float4 hi, float& nearv) const
     {
-#if PTG_PK_SLAB
-        const v2f tx = (v2f{lo.x, hi.x} - v2f{org.x, org.x}) * v2f{inv.x, inv.x};
-        const v2f ty = (v2f{lo.y, hi.y} - v2f{org.y, org.y}) * v2f{inv.y, inv.y};
-        const v2f tz = (v2f{lo.z, hi.z} - v2f{org.z, org.z}) * v2f{inv.z, inv.z};
-        const float t0x = tx.x, t1x = tx.y, t0y = ty.x, t1y = ty.y, t0z = tz.x, t1z = tz.y;
-#else
         const float t0x = (lo.x - org.x) * inv.x, t1x = (hi.x - org.x) * inv.x;
         const float t0y = (lo.y - org.y) * inv.y, t1y = (hi.y - org.y) * inv.y;
         const float t0z = (lo.z - org.z) * inv.z, t1z = (hi.z - org.z) * inv.z;
-#endif
         nearv = fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z)));
         const float farv = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
         return nearv <= farv && farv > tmin && nearv < tmax;
@@ -459,28 +388,20 @@ struct BlockWalker {
         inst = leaf;
         bsp = st.size();
         oct = octant(bd);
-#if PTG_FAST_RCP
         bool ok = true;   // one fallback branch for the four reciprocals of the entry
         inv = V3(rcp_nr(bd.x, ok), rcp_nr(bd.y, ok), rcp_nr(bd.z, ok));
-#else
-        inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
-#endif
         // ray_triangle_intersection_preprocess (math.hh:340-356)
         const float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
         f3 rd = bd;
         axis = 2;
         if(ax > ay && ax > az) { axis = 0; rd = V3(bd.z, bd.y, bd.x); }
         else if(ay > az) { axis = 1; rd = V3(bd.x, bd.z, bd.y); }
-#if PTG_FAST_RCP
         float k = rcp_nr(rd.z, ok);
         if(!ok)
         {   // a zero, denormal or huge component (rare): IEEE division
             inv = V3(rcp_or_big(bd.x), rcp_or_big(bd.y), rcp_or_big(bd.z));
             k = 1.0f / rd.z;
         }
-#else
-        const float k = 1.0f / rd.z;
-#endif
         S = V3(rd.x * k, rd.y * k, 1.0f * k);
         fin = finite3(inv);
     }
@@ -506,7 +427,7 @@ struct BlockWalker {
     // whether the leaf phase has work: a parked triangle, or a leaf in cur
     PTG_D bool wants_leaf() const { return pend != kBePop || at_leaf(); }
 
-    // PTG_PEND: a triangle the walk reaches is parked (with its near) while
+    // A triangle the walk reaches is parked (with its near) while
     // the walk goes on with its next node steps; the leaf phase tests it.
     // Triangles are still tested in the walk's order, each after a near <
     // tmax re-check at its own time, and tmax changes only at triangle tests:
@@ -515,14 +436,12 @@ struct BlockWalker {
     // never parked, and a walk with a parked triangle does not leave its BLAS.
     PTG_D void park()
     {
-#if PTG_PEND
         if(axis >= 0 && pend == kBePop && at_leaf())
         {
             pend = cur;
             pnear = cnear;
             cur = kBePop;
         }
-#endif
     }
 
     // Node phase, first half: pop the next entry if the walk needs one.
@@ -640,11 +559,7 @@ struct BlockWalker {
     PTG_D LeafSel leaf_select(const DevScene& sc)
     {
         LeafSel ls;
-#if PTG_PEND
         ls.parked = pend != kBePop;
-#else
-        ls.parked = false;
-#endif
         ls.id = (ls.parked ? pend : cur) & kBeIndex;
         const float n = ls.parked ? pnear : cnear;
         if(ls.parked) pend = kBePop;
@@ -696,47 +611,6 @@ struct BlockWalker {
             r0 = ls.p[0]; r1 = ls.p[1]; r2 = ls.p[2]; r3 = ls.p[3];
         }
         return leaf_finish<ANY, COUNT>(sc, cnt, ls, r0, r1, r2, r3);
-    }
-
-    // PTG_WALK_SCHED 1: one step of either kind - the lane's leaf work if it
-    // has any, else a node step - with both kinds' rows read by the same
-    // seven loads (a leaf lane's last three rows are unused; the record
-    // buffers carry the slack), so a wave with lanes of both kinds waits for
-    // memory once.  Returns as node_step / leaf_step.
-    template<bool ANY, bool COUNT>
-    PTG_D int mixed_step(const DevScene& sc, Counters& cnt)
-    {
-        const bool lf = wants_leaf();
-        LeafSel ls{nullptr, 0, false, false, false};
-        int nr = -1;
-        const v4f* p = nullptr;
-        bool load;
-        if(lf)
-        {
-            ls = leaf_select(sc);
-            if(ls.inst_leaf) PTG_CHECK(sc, ls.id < sc.inst_count, kDebugInst);
-            if(ls.tri) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);
-            p = ls.p;
-            load = ls.inst_leaf || ls.tri;
-        }
-        else
-        {
-            nr = node_pop();
-            load = nr < 0;
-            if(load)
-            {
-                PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
-                p = block_rows(sc);
-            }
-        }
-        v4f q0 = {0, 0, 0, 0}, q1 = q0, q2 = q0, q3 = q0, q4 = q0, q5 = q0, q6 = q0;
-        if(load)
-        {
-            q0 = p[0]; q1 = p[1]; q2 = p[2]; q3 = p[3]; q4 = p[4]; q5 = p[5]; q6 = p[6];
-        }
-        if(lf) return leaf_finish<ANY, COUNT>(sc, cnt, ls, q0, q1, q2, q3);
-        if(nr >= 0) return nr;
-        return node_block<COUNT>(sc, cnt, q0, q1, q2, q3, q4, q5, q6);
     }
 
     // One step of either phase (the per-lane walks: the megakernel and the
@@ -1238,9 +1112,6 @@ PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     float tmin = 0, atmax = 0;
-#ifdef PTG_ABLATE_ATMO
-    return V3(1.0f, 1.0f, 1.0f);
-#endif
     if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return V3(1.0f, 1.0f, 1.0f);
     tmin = (float)gmax_d((double)tmin, 0.0);
     tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
@@ -1267,9 +1138,6 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     attenuation = V3(1.0f, 1.0f, 1.0f);
     in_scatter = V3(0.0f, 0.0f, 0.0f);
-#ifdef PTG_ABLATE_ATMO
-    return;
-#endif
     if(tmax > 0 && tmax < 1e3f) return;
     float tmin = 0, atmax = 0;
     if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return;

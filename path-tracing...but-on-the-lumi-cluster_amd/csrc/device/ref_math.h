@@ -103,14 +103,8 @@ PTG_D float sqrt_rn(float x)
 }
 
 // f32 sqrt: correctly rounded == the reference's (float)sqrt((double)x)
-#ifndef PTG_FAST_SQRT
-#define PTG_FAST_SQRT 0   // measured: sky kernel slower with sqrt_rn (frame 0 +1%), see DESIGN.md
-#endif
-#if PTG_FAST_SQRT
-PTG_D float fsqrt(float x) { return sqrt_rn(x); }
-#else
+// (sqrt_rn here measured slower in the sky kernel: frame 0 +1%)
 PTG_D float fsqrt(float x) { return __builtin_sqrtf(x); }
-#endif
 PTG_D float length(f3 a) { return fsqrt(dot(a, a)); }
 PTG_D f3 normalize(f3 a) { return a / length(a); }
 
@@ -128,21 +122,12 @@ PTG_D float signf(float v)
 }
 
 // double-precision library calls, as the reference makes them
-#ifdef PTG_ABLATE_FASTMATH   // timing ablation only: single-precision hardware approximations
-PTG_D double dexp(double x) { return __expf((float)x); }
-PTG_D double dlog(double x) { return __logf((float)x); }
-PTG_D double dpow(double x, double y) { return __powf((float)x, (float)y); }
-PTG_D double dsin(double x) { return __sinf((float)x); }
-PTG_D double dcos(double x) { return __cosf((float)x); }
-PTG_D double dsqrt(double x) { return __fsqrt_rn((float)x); }
-#else
 PTG_D double dexp(double x) { return exp(x); }
 PTG_D double dlog(double x) { return log(x); }
 PTG_D double dpow(double x, double y) { return pow(x, y); }
 PTG_D double dsin(double x) { return sin(x); }
 PTG_D double dcos(double x) { return cos(x); }
 PTG_D double dsqrt(double x) { return sqrt(x); }
-#endif
 PTG_D float fcos(float x) { return (float)dcos((double)x); }
 PTG_D float fsin(float x) { return (float)dsin((double)x); }
 PTG_D float fexp(float x) { return (float)dexp((double)x); }

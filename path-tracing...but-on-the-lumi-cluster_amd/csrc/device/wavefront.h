@@ -74,8 +74,10 @@ struct PathRec {
 
 PTG_D f3 xyz(float4 v) { return V3(v.x, v.y, v.z); }
 
-#if PTG_NT_STATE >= 2
-// path state read and written once per round: non-temporal (PTG_NT_STATE 2)
+// Path state, trace results and per-sample results pass through once per
+// round: non-temporal (streaming) accesses, so they do not evict BVH records
+// from L2 and the Infinity Cache (measured at 1024 spp: frame 0 -1.3%,
+// frame 450 -1.1%).
 template<typename T> PTG_D T ld_state(const T* p)
 {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -91,18 +93,9 @@ template<typename T> PTG_D void st_state(T* p, T value)
     __builtin_memcpy(&v, &value, 16);
     __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
 }
-#else
-template<typename T> PTG_D T ld_state(const T* p) { return *p; }
-template<typename T> PTG_D void st_state(T* p, T value) { *p = value; }
-#endif
 // per-sample results (written once by shade / sky / camera, read once by k_accumulate)
-#if PTG_NT_STATE >= 3
 template<typename T> PTG_D T ld_out(const T* p) { return ld_state(p); }
 template<typename T> PTG_D void st_out(T* p, T value) { st_state(p, value); }
-#else
-template<typename T> PTG_D T ld_out(const T* p) { return *p; }
-template<typename T> PTG_D void st_out(T* p, T value) { *p = value; }
-#endif
 
 PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
 {
@@ -113,9 +106,7 @@ PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
     st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
     st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
     st_state(S.batt + q, make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f));
-#if PTG_NEE_LAZY >= 2
     if(!meta_nee(p.meta)) return;   // no pending NEE ray: its records are never read
-#endif
     st_state(S.nee_c + q, make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf));
     st_state(S.nee_d + q, make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter));
 }
@@ -138,7 +129,6 @@ PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
         p.nee = NeeCandidate{V3(0, 0, 0), V3(0, 0, 0), 0, 0};
         return p;
     }
-#if PTG_NEE_LAZY
     // the pending NEE candidate is read only by paths that have one (classify
     // groups those paths together, so a wave mostly takes one side)
     float4 nc = make_float4(0.f, 0.f, 0.f, 0.f), nd = nc;
@@ -148,10 +138,6 @@ PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
         nd = ld_state(S.nee_d + q);
     }
     const float4 a = ld_state(S.att + q), c = ld_state(S.contrib + q);
-#else
-    const float4 a = ld_state(S.att + q), c = ld_state(S.contrib + q), nc = ld_state(S.nee_c + q),
-                 nd = ld_state(S.nee_d + q);
-#endif
     p.att = xyz(a);
     p.reg = a.w;
     p.contrib = xyz(c);

@@ -396,7 +396,7 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
                                     part[i], pinfo[i], perr[i]);
         }
     };
-    const size_t nthreads = std::min<size_t>(subframe_count, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+    const size_t nthreads = std::min<size_t>(subframe_count, std::min(8u, host_threads()));
     if(nthreads > 1)
     {
         std::vector<std::thread> pool;

@@ -7,6 +7,8 @@
 
 namespace ptg {
 
+unsigned host_threads();   // scene.cpp: this process's share of the host's CPUs
+
 struct BlockBvh {
     uint32_t root = 0;          // root block index (absolute: block_base + position)
     uint32_t blocks = 0;        // blocks appended

@@ -19,11 +19,39 @@
 #include <sstream>
 #include <stdexcept>
 #include <thread>
+#include <sched.h>
 
 namespace ptg {
 
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+static std::atomic<unsigned> g_host_threads{0};   // ptg_set_host_threads; 0 = automatic
+
+unsigned host_threads()
+{
+    if(const unsigned n = g_host_threads.load()) return n;
+    static const unsigned automatic = [] {
+        unsigned cpus = std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if(sched_getaffinity(0, sizeof(set), &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+        // cgroup v2 quota "max 100000" or "<quota> <period>" (a job limited to
+        // N CPUs of time runs N-ish threads at full speed, not more)
+        if(FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r"))
+        {
+            char q[32] = {0};
+            long period = 0;
+            if(fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+                cpus = std::min(cpus, unsigned(std::max(1L, (atol(q) + period - 1) / period)));
+            fclose(f);
+        }
+        // ranks of one node share the host (torch.distributed.run sets it)
+        if(const char* lw = getenv("LOCAL_WORLD_SIZE"))
+            if(const int ranks = atoi(lw); ranks > 1) cpus = std::max(1u, cpus / unsigned(ranks));
+        return cpus;
+    }();
+    return automatic;
+}
 
 namespace {
 
@@ -204,9 +232,7 @@ void load_meshes_parallel(ptg_scene& s, const std::string& assets)
         std::string error;
     };
     std::vector<Part> parts(kCount);
-    size_t threads = std::thread::hardware_concurrency();
-    if(const char* e = std::getenv("PTG_LOAD_THREADS")) threads = size_t(std::max(1, atoi(e)));
-    threads = std::max<size_t>(1, std::min<size_t>(threads ? threads : 1, std::min<size_t>(kCount, 16)));
+    const size_t threads = std::max<size_t>(1, std::min<size_t>(host_threads(), std::min<size_t>(kCount, 16)));
     std::atomic<size_t> next{0};
     auto worker = [&] {
         // biggest meshes are not first in the list; a shared counter balances them
@@ -400,8 +426,7 @@ void setup_frame(ptg_scene& s, uint32_t frame_index)
         for(uint32_t k = dynamic[i].first; k < dynamic[i].second; ++k) { list.push_back(&s.instances[k]); ids.push_back(k); }
         s.subframes[i].tlas = build_tlas(list.size(), list.data(), ids.data(), s.bvh_buf, local[i]);
     };
-    unsigned nt = std::max(1u, std::min(count, std::thread::hardware_concurrency()));
-    nt = std::min(nt, 16u);
+    const unsigned nt = std::max(1u, std::min(std::min(count, host_threads()), 16u));
     std::vector<std::thread> pool;
     for(unsigned w = 0; w < nt; ++w)
         pool.emplace_back([&, w] { for(uint32_t i = w; i < count; i += nt) build_one(i); });
@@ -436,6 +461,13 @@ void ptg_render_config_default(ptg_render_config* cfg)
 
 int ptg_abi_version(void) { return PTG_ABI_VERSION; }
 const char* ptg_last_error(void) { return ptg::g_last_error.c_str(); }
+
+int ptg_set_host_threads(int threads)
+{
+    if(threads < 0) { ptg::set_last_error("ptg_set_host_threads: negative"); return PTG_E_INVALID; }
+    ptg::g_host_threads.store(unsigned(threads));
+    return int(ptg::host_threads());
+}
 
 int ptg_scene_load(const char* assets_dir, const ptg_render_config* cfg, ptg_scene** out)
 {

@@ -70,4 +70,9 @@ struct ptg_scene {
 
 namespace ptg {
 void set_last_error(const std::string& msg);
+// Host worker threads one of this process's pools may use: the CPUs this
+// process may run on (affinity mask, cgroup CPU quota) shared by the ranks of
+// one node (LOCAL_WORLD_SIZE, set by torch.distributed.run), at least 1;
+// ptg_set_host_threads overrides it.
+unsigned host_threads();
 }

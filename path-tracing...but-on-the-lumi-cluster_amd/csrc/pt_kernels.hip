@@ -40,9 +40,7 @@ using namespace ptg::dm;
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef PTG_SHADE_WAVES
 #define PTG_SHADE_WAVES 2
-#endif
 
 // ---------------------------------------------------------------- kernels --
 
@@ -206,48 +204,32 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the grid is sized to what is resident, each wave owns a contiguous range of
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
-#ifndef PTG_REFILL_IDLE
-#define PTG_REFILL_IDLE 24
-#endif
-constexpr int kRefillIdle = PTG_REFILL_IDLE;   // refill once at least this many lanes are idle
-#ifndef PTG_WALK_WAVES
-#define PTG_WALK_WAVES 5    // VGPR cap 96 (closest-hit walk: 104 uncapped, no spills at 96): the LDS holds 4 walk
-                            // blocks per CU, and the registers left beside them take a sky wave and more of shade
-#endif
-#ifndef PTG_SHADOW_WAVES
-#define PTG_SHADOW_WAVES 6  // the any-hit walk fits 80 VGPRs without spills (76): a shade wave (160) fits beside it
-#endif
+constexpr int kRefillIdle = 24;   // refill once at least this many lanes are idle (16 / 32: slower)
+// waves per SIMD the walks are compiled for: the closest-hit walk at 96 VGPRs
+// (104 uncapped, no spills at 96), the any-hit walk at 80 (76 used), so a
+// shade wave (160) fits beside it
+#define PTG_WALK_WAVES 5
+#define PTG_SHADOW_WAVES 6
 #define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(ANY ? PTG_SHADOW_WAVES : PTG_WALK_WAVES, 8)))
-#ifndef PTG_WALK_UNROLL
-#define PTG_WALK_UNROLL 2   // node steps per leaf phase (block walker, 256 spp: 2 beats 1 by 1-3% and 3 by 2-5%, 4 is slower)
-#endif
-#ifndef PTG_WALK_SCHED
-#define PTG_WALK_SCHED 0    // 0: node phases then a leaf phase; 1: a step of either kind, then a node step (slower, kept as an option)
-#endif
-#ifndef PTG_VMEM_STATS
-#define PTG_VMEM_STATS 0
-#endif
-#ifndef PTG_WF_SLOTS
-#define PTG_WF_SLOTS 2      // concurrent wavefront chunk pipelines (ptg_context::Slot)
-#endif
-#ifndef PTG_WALK_REGCOLD
-#define PTG_WALK_REGCOLD 0  // 1: the walk's world ray and best hit in registers, only the stack in LDS
-#endif
-#ifndef PTG_WALK_RESIDENT
-#define PTG_WALK_RESIDENT 4 // walk blocks per CU (LDS-bound with 16-entry stack windows: 4 x 40 KB)
-#endif
-#ifndef PTG_WALK_BLOCKS_PER_CU
-#define PTG_WALK_BLOCKS_PER_CU 3   // walk grid: blocks per CU (0: all that are resident); see ptg_context_create
-#endif
-#ifndef PTG_XCD_BANDS
-#define PTG_XCD_BANDS 1024
-#endif
-constexpr uint32_t kBands = PTG_XCD_BANDS;   // a multiple of the XCD count (8 on MI355X)
+constexpr int kWalkUnroll = 2;     // node steps per leaf phase (1 and 3 measured slower)
+constexpr uint32_t kWalkResident = 4;      // walk blocks the LDS holds per CU (16-entry stack windows: 4 x 40 KB)
+constexpr uint32_t kWalkBlocksPerCu = 3;   // walk grid: blocks per CU (one resident wave, see ptg_context_create)
+constexpr uint32_t kWfSlots = 2;           // concurrent wavefront chunk pipelines (ptg_context::Slot)
+constexpr uint32_t kBands = 1024;   // XCD bands of a walk queue: a multiple of the XCD count (8 on MI355X)
+
+// Walk statistics of the counting build (per walk kind, see WalkStats): how
+// many lanes each vector-memory instruction of the walk serves.  The walk's
+// vector-memory issue costs the same per wave instruction whatever its EXEC
+// mask (profiles/r02_probe/ta_probe.txt), so lanes per instruction is the
+// lever on that level.
+enum WalkStat : int { WS_NODE_WAVES = 0, WS_NODE_LANES, WS_LEAF_WAVES, WS_LEAF_LANES, WS_REFILL_WAVES,
+                      WS_REFILL_LANES, WS_ITERS, WS_ACTIVE_LANES, WS_COUNT };
 
 template<bool ANY, bool COUNT>
 __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, PathSoA S, const uint32_t* __restrict__ counts,
                                                     uint32_t round, const uint32_t* __restrict__ list, TraceOut tr,
-                                                    uint32_t nxcd, unsigned long long* __restrict__ counters)
+                                                    uint32_t nxcd, unsigned long long* __restrict__ counters,
+                                                    unsigned long long* __restrict__ wstats)
 {
     const uint32_t n = counts[2 * round + (ANY ? 1 : 0)];
     const uint32_t lane = threadIdx.x & 63u;
@@ -268,48 +250,37 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
     Counters cnt;
-#if PTG_WALK_REGCOLD
-    // LDS: the stack windows, one 64-lane x kCap entry table per wave; the
-    // world ray and best hit stay in registers
-    extern __shared__ uint2 walk_lds[];
-    BlockWalker<LeanCold, LdsStack> w;
-    w.st.s = (lds_uint2_t*)(walk_lds + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);   // C cast: generic -> LDS
-#else
     // LDS: every lane's world ray, then the stack windows, one 64-lane x kCap
     // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
     BlockWalker<LdsCold, LdsStack> w;
     w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C casts: generic -> LDS address space
     w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);
-#endif
     w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
     bool active = false;
     uint32_t q = 0;
-    // a finished walk writes its result: the shadow flag, or the closest hit
+    // a finished walk writes its result: the shadow flag, or the closest hit;
+    // results stream once through the caches (non-temporal), so they do not
+    // evict BVH records from L2 / the Infinity Cache
     auto finish = [&](int r) {
-#if PTG_NT_STATE
         if(ANY) __builtin_nontemporal_store(r == 2 ? 1u : 0u, tr.shadow + q);
-#else
-        if(ANY) tr.shadow[q] = r == 2 ? 1u : 0u;
-#endif
         else
         {
             const Hit h = w.result();
-#if PTG_NT_STATE
             nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
-#if PTG_MISS_BARY
             if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
-#endif
                 nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
-#else
-            tr.hit[q] = make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u);
-            tr.bary[q] = make_float4(h.bx, h.by, h.bz, 0.f);
-#endif
         }
     };
-#if PTG_VMEM_STATS
-    uint32_t vm_rec = 0, vm_tri = 0, vm_inst = 0, vm_refill = 0;
-#endif
+    unsigned long long ws[WS_COUNT] = {};   // COUNT: lane 0's tallies for its wave
+    auto tally = [&](int waves_slot, bool loads) {
+        const unsigned long long m = __ballot(loads);
+        if(lane == 0 && m)
+        {
+            ws[waves_slot] += 1;
+            ws[waves_slot + 1] += (unsigned long long)__popcll(m);
+        }
+    };
     for(;;)
     {
         if(cursor < end)
@@ -318,9 +289,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if(nidle >= (uint32_t)kRefillIdle || nidle == 64u)
             {
-#if PTG_VMEM_STATS
-                if(COUNT && lane == 0) vm_refill++;
-#endif
+                bool took = false;
                 if(!active)
                 {
                     const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
@@ -336,83 +305,59 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                         if(!bad)
 #endif
                         {
-#if PTG_NT_STATE
-                            // path state streams once through the caches: non-temporal, so it
-                            // does not evict BVH records from L2 / the Infinity Cache
+                            // path state streams once through the caches: non-temporal
                             const uint4 m = nt_load(S.meta + q);
                             w.init(m.z, xyz(nt_load(S.ray_o + q)),
                                    ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)), tmin, tmax);
-#else
-                            const uint4 m = S.meta[q];
-                            w.init(m.z, xyz(S.ray_o[q]), ANY ? xyz(S.nee_d[q]) : xyz(S.ray_d[q]), tmin, tmax);
-#endif
                             active = true;
+                            took = true;
                             if(COUNT) cnt.queries++;
                         }
                     }
                 }
+                if(COUNT) tally(WS_REFILL_WAVES, took);
                 cursor = min(end, cursor + nidle);
             }
         }
         if(!__any(active)) break;
-        if(COUNT && lane == 0) cnt.iters++;   // wave loop iterations (lane 0 counts for its wave)
-        // Node phase, up to PTG_WALK_UNROLL block steps (each after the pop it
+        if(COUNT)
+        {
+            const unsigned long long m = __ballot(active);
+            if(lane == 0)
+            {
+                ws[WS_ITERS] += 1;
+                ws[WS_ACTIVE_LANES] += (unsigned long long)__popcll(m);
+                cnt.iters++;
+            }
+        }
+        // Node phase, up to kWalkUnroll block steps (each after the pop it
         // needs), for lanes not standing at a leaf; then one leaf phase for the
         // lanes that are.  The leaf code (triangle test, BLAS entry) then runs
         // once per iteration with many lanes, not once per block step with few.
         int r = 0;
-#if PTG_WALK_SCHED == 1
-        // a step of either kind (leaf work first), then a node step
-        if(active)
-        {
-            r = w.template mixed_step<ANY, COUNT>(sc, cnt);
-            if(r != 0) { finish(r); active = false; r = 0; }
-        }
-        if(active && !w.at_leaf())
-        {
-            r = w.template node_step<COUNT>(sc, cnt);
-            if(r != 0) { finish(r); active = false; }
-        }
-        continue;
-#endif
 #pragma unroll
-        for(int u = 0; u < PTG_WALK_UNROLL; ++u)
+        for(int u = 0; u < kWalkUnroll; ++u)
         {
-#if PTG_VMEM_STATS
             if(COUNT) cnt.step_loads = 0;
-#endif
             if(active && !w.at_leaf()) r = w.template node_step<COUNT>(sc, cnt);   // (a lane with a parked triangle walks on)
-#if PTG_VMEM_STATS
-            if(COUNT)
-            {
-                const unsigned long long br = __ballot(cnt.step_loads & 1u);
-                if(lane == 0) vm_rec += br != 0;
-            }
-#endif
+            if(COUNT) tally(WS_NODE_WAVES, (cnt.step_loads & 1u) != 0);
             if(active && r != 0) { finish(r); active = false; r = 0; }
         }
-#if PTG_VMEM_STATS
         if(COUNT) cnt.step_loads = 0;
-#endif
         if(active && w.wants_leaf())
         {
             r = w.template leaf_step<ANY, COUNT>(sc, cnt);
             if(r != 0) { finish(r); active = false; }
         }
-#if PTG_VMEM_STATS
-        if(COUNT)
-        {
-            const unsigned long long bt = __ballot(cnt.step_loads & 2u), bi = __ballot(cnt.step_loads & 4u);
-            if(lane == 0) { vm_tri += bt != 0; vm_inst += bi != 0; }
-        }
-#endif
+        if(COUNT) tally(WS_LEAF_WAVES, (cnt.step_loads & 6u) != 0);
     }
-#if PTG_VMEM_STATS
-    if(COUNT) { cnt.shades = vm_tri; cnt.tlas_visits = vm_inst; cnt.iters = vm_refill; }
-    if(COUNT) flush_counters(cnt, counters, vm_rec);
-#else
-    if(COUNT) flush_counters(cnt, counters, 0);
-#endif
+    if(COUNT)
+    {
+        flush_counters(cnt, counters, 0);
+        if(lane == 0)
+            for(int k = 0; k < WS_COUNT; ++k)
+                if(ws[k]) atomicAdd(wstats + k, ws[k]);
+    }
 }
 
 // Shading of one round is split by what the paths will run.
@@ -426,7 +371,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
 // atmosphere integrals - runs in its own small kernel at high occupancy.
 // Which lane shades which path has no effect on the result.
 __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
-                                                        const uint4* __restrict__ meta, uint32_t* __restrict__ hit_list,
+                                                        uint32_t* __restrict__ hit_list,
                                                         uint32_t* __restrict__ sky_list, uint32_t* __restrict__ lcounts)
 {
     // Each block deals a tile of kTile entries with ONE 64-bit atomic on the
@@ -451,13 +396,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
             if(q < n)
             {
                 const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
-#if PTG_CLASSIFY_FLAG
                 // shade(round-1) wrote 1 for survivors without a pending NEE ray,
                 // the shadow walk 0/1 for those with one (meta is not read)
                 const bool nee = round > 0 && tr.shadow[q] == 0;
-#else
-                const bool nee = round > 0 && meta_nee(meta[q]) && tr.shadow[q] == 0;
-#endif
                 key[k] = (hit ? 2u : 0u) | (nee ? 1u : 0u);
                 rank[k] = atomicAdd(&bin_count[key[k]], 1u);
             }
@@ -486,14 +427,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
 // it on the sky list because its hit distance was not positive).  The walk
 // reports such a ray as WalkerT::result() does, thit = -1 and no hit, and the
 // sky branch of shade_path reads nothing else of it: the hit and barycentric
-// records are not fetched (nor, PTG_MISS_BARY, the barycentrics written).
+// records are not fetched (nor the barycentrics written by the walk).
 template<bool MISS = false>
 __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& tr, uint32_t q, PathRec& p, Hit& h,
                                             bool& occluded, bool carried)
 {
     p = load_path(cur, q, carried);
     occluded = meta_nee(p.meta) ? tr.shadow[q] != 0 : false;
-#if PTG_MISS_BARY
     if(MISS)
     {
         h.thit = -1.0f;
@@ -503,7 +443,6 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
         h.bx = h.by = h.bz = 0.0f;
         return;
     }
-#endif
     const uint4 hv = ld_state(tr.hit + q);
     const float4 bv = ld_state(tr.bary + q);
     h.thit = __uint_as_float(hv.x);
@@ -568,9 +507,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         const uint32_t qn = blk_base + oct_start[okey] + orank;
         if(cont) store_path(nxt, qn, p);
         if(nee) next_list[nee_base + nrank] = qn;
-#if PTG_CLASSIFY_FLAG
         else if(cont) __builtin_nontemporal_store(1u, next_shadow + qn);   // no NEE ray: k_wf_classify reads "occluded"
-#endif
         __syncthreads();   // the LDS tables are rewritten by the next iteration
     }
     if(COUNT) flush_counters(cnt, counters, 0);
@@ -578,9 +515,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
 // (path_tracer.hh:456-588), retire.  No survivors.
-#ifndef PTG_SKY_WAVES
 #define PTG_SKY_WAVES 5     // 96 VGPRs, no spills (at 8 waves / 64 VGPRs it spilled 49): fits beside 4 walk waves per SIMD
-#endif
 #define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr, uint32_t round,
@@ -824,18 +759,17 @@ struct ptg_context {
     int pipeline = 0;
     uint32_t persistent_blocks = 2048;
     uint32_t walk_grid[2] = {2048, 2048};
-    uint32_t walk_grid_r0 = 2048;          // closest-hit walk grid of round 0 (camera rays)
-    bool sky_early = false;                // PTG_SKY_EARLY (experiments)
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
-    uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (PTG_HBM_PCT)
-    // wavefront: <= 2^chunk_log2 live paths per chunk (PTG_CHUNK_LOG2).  2^27
-    // paths x 392 B = 53 GB per pipeline, ~37% of an MI355X's HBM for the two
-    // pipelines together, so a default render leaves most of the GPU to other
-    // tenants; 2^28 (73%) is 1-3% faster on a GPU the renderer owns alone.
+    uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (ptg_set_hbm_share)
+    // wavefront: <= 2^chunk_log2 live paths per chunk.  2^27 paths x 392 B =
+    // 53 GB per pipeline, ~37% of an MI355X's HBM for the two pipelines
+    // together, so a default render leaves most of the GPU to other tenants;
+    // 2^28 (73%) is 1-3% faster on a GPU the renderer owns alone.
     uint32_t chunk_log2 = 27;
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
+    uint64_t walk_stats[2][8] = {};        // counting builds: WalkStat tallies of the closest-hit / any-hit walks
     // second stream for the sky kernels + the events that order it with `stream`
     hipStream_t side = nullptr;
     hipEvent_t ev_main = nullptr, ev_side = nullptr;
@@ -847,13 +781,11 @@ struct ptg_context {
     struct Slot {
         hipStream_t main = nullptr, side = nullptr;
         hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_done = nullptr, ev_acc = nullptr;
-        hipStream_t shd = nullptr;     // experiments (PTG_SHADOW_STREAM): the any-hit walk on its own stream
-        hipEvent_t ev_shd = nullptr;
         DevBuf own_state, own_samples;
         DevBuf* state = nullptr;
         DevBuf* samples = nullptr;
     };
-    static constexpr uint32_t kMaxSlots = 3;
+    static constexpr uint32_t kMaxSlots = kWfSlots;
     Slot slot[kMaxSlots];
     uint32_t nslots = 1;
     uint32_t concurrency = 2;              // ptg_set_concurrency
@@ -874,15 +806,38 @@ struct ptg_context {
         }
         for(uint32_t k = 0; k < kMaxSlots; ++k)
         {
-            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc, slot[k].ev_shd})
+            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc})
                 if(e) (void)hipEventDestroy(e);
-            if(slot[k].shd) (void)hipStreamDestroy(slot[k].shd);
         }
         for(hipEvent_t e: {ev_render_start, ev_acc_end})
             if(e) (void)hipEventDestroy(e);
         if(acc_stream) (void)hipStreamDestroy(acc_stream);
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
         for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
+    }
+
+    // Wait for everything queued on the context's streams: the caller's
+    // stream, the second streams, the extra chunk pipeline and the
+    // accumulation stream.
+    hipError_t drain() const
+    {
+        for(hipStream_t st: {stream, side, acc_stream})
+            if(hipError_t e = hipStreamSynchronize(st)) return e;
+        for(uint32_t k = 1; k < kMaxSlots; ++k)
+            for(hipStream_t st: {slot[k].main, slot[k].side})
+                if(st)
+                    if(hipError_t e = hipStreamSynchronize(st)) return e;
+        return hipSuccess;
+    }
+    // Grow a workspace buffer.  Growing frees the old allocation, which work
+    // still queued on the context's streams may read: drain them first (rare,
+    // the buffers only grow), rather than rely on hipFree's implicit sync.
+    hipError_t grow(DevBuf& b, size_t n) const
+    {
+        if(n <= b.bytes && b.p) return hipSuccess;
+        if(b.p)
+            if(hipError_t e = drain()) return e;
+        return b.reserve(n);
     }
 
     DevScene scene_args(const ptg_render_config* cfg) const
@@ -946,6 +901,9 @@ int check_cfg(const ptg_context* ctx, const ptg_render_config* cfg, uint32_t sam
 // separately and count into K_SHADE)
 enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA = 4, K_ACCUM = 5, K_KINDS = 6,
                   K_SKY = 6, K_CLASSIFY = 7 };
+// counting builds: 8 work counters per kind, then WS_COUNT walk statistics
+// for the closest-hit and the any-hit walk
+constexpr int kCounterWords = K_KINDS * 8 + 2 * WS_COUNT;
 
 int timed_begin(ptg_context* ctx, int kind, hipStream_t st = nullptr);
 int timed_end(ptg_context* ctx, hipStream_t st = nullptr);
@@ -1005,13 +963,13 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const size_t M = size_t((pm.npix + 7) / 8) * ((chunk + 7) / 8) * 64;   // lanes per chunk (upper bound)
     if(M >= (1ull << 31)) return fail(PTG_E_RANGE, "chunk too large");
     for(uint32_t k = 0; k < nslots; ++k)
-        PTG_HIP(slots[k].samples->reserve(size_t(pm.npix) * chunk * sizeof(float4)));
-    PTG_HIP(ctx->acc.reserve(size_t(pm.npix) * sizeof(float4)));
+        PTG_HIP(ctx->grow(*slots[k].samples, size_t(pm.npix) * chunk * sizeof(float4)));
+    PTG_HIP(ctx->grow(ctx->acc, size_t(pm.npix) * sizeof(float4)));
     unsigned long long* cnt_dev = nullptr;
     if(ctx->counting)
     {
-        PTG_HIP(ctx->counters.reserve(K_KINDS * 8 * sizeof(unsigned long long)));
-        PTG_HIP(hipMemsetAsync(ctx->counters.p, 0, K_KINDS * 8 * sizeof(unsigned long long), ctx->stream));
+        PTG_HIP(ctx->grow(ctx->counters, kCounterWords * sizeof(unsigned long long)));
+        PTG_HIP(hipMemsetAsync(ctx->counters.p, 0, kCounterWords * sizeof(unsigned long long), ctx->stream));
         cnt_dev = ctx->counters.as<unsigned long long>();
     }
     const uint32_t rounds = cfg->max_bounces + 1;
@@ -1027,7 +985,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         for(uint32_t k = 0; k < nslots; ++k)
         {
             const size_t rec = M * 16;
-            PTG_HIP(slots[k].state->reserve(2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
             char* b = slots[k].state->as<char>();
             SlotState& t = st[k];
             for(int h = 0; h < 2; ++h)
@@ -1064,8 +1022,8 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const DevScene sc = ctx->scene_args(cfg);
     // walk stack spill areas: one per (chunk pipeline, walk kind), since up to
     // four walk launches run at once; stack_bound entries per walk lane
-    const size_t spill_region = size_t(std::max({ctx->walk_grid[0], ctx->walk_grid[1], ctx->walk_grid_r0})) * kBlock * ctx->stack_bound;
-    if(wf) PTG_HIP(ctx->spill.reserve(std::max<size_t>(1, 2 * nslots * spill_region) * sizeof(uint2)));
+    const size_t spill_region = size_t(std::max(ctx->walk_grid[0], ctx->walk_grid[1])) * kBlock * ctx->stack_bound;
+    if(wf) PTG_HIP(ctx->grow(ctx->spill, std::max<size_t>(1, 2 * nslots * spill_region) * sizeof(uint2)));
     auto walk_scene = [&](uint32_t slot, int kind) {
         DevScene w = sc;
         w.spill = ctx->spill.as<uint2>() + (2 * slot + uint32_t(kind)) * spill_region;
@@ -1074,6 +1032,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const uint32_t persistent = ctx->persistent_blocks;
     const bool overlap = wf && ctx->side != nullptr && ctx->concurrency >= 1;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
+    auto ws_for = [&](bool any) { return cnt_dev ? cnt_dev + 8 * K_KINDS + (any ? WS_COUNT : 0) : nullptr; };
     uint32_t chunk_index = 0;
     for(uint32_t j = j0; j < j1; j += chunk, ++chunk_index)
     {
@@ -1124,33 +1083,28 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 const TraceOut& tr = trs[r & 1];
                 if(int e = timed_begin(ctx, K_EXTEND, ms)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL((k_wf_walk<false, true>), r ? ctx->walk_grid[0] : ctx->walk_grid_r0, dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
-                                       counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND));
+                    hipLaunchKernelGGL((k_wf_walk<false, true>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext,
+                                       cur, counts, r, nullptr, tr, ctx->walk_xcds[0], cnt_for(K_EXTEND), ws_for(false));
                 else
-                    hipLaunchKernelGGL((k_wf_walk<false, false>), r ? ctx->walk_grid[0] : ctx->walk_grid_r0, dim3(kBlock), ctx->walk_lds[0], ms, sc_ext, cur,
-                                       counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr);
+                    hipLaunchKernelGGL((k_wf_walk<false, false>), ctx->walk_grid[0], dim3(kBlock), ctx->walk_lds[0], ms, sc_ext,
+                                       cur, counts, r, nullptr, tr, ctx->walk_xcds[0], nullptr, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
                 // second stream: the previous round's sky kernel, then this round's
                 // shadow walk (independent of the closest-hit walk it runs beside)
-                hipStream_t ss = overlap ? sl.side : ms;
-                const hipStream_t shs = (overlap && sl.shd) ? sl.shd : ss;   // the any-hit walk's stream
+                const hipStream_t ss = overlap ? sl.side : ms;
                 if(r > 0)
                 {
-                    if(int e = timed_begin(ctx, K_SHADOW, shs)) return e;
+                    if(int e = timed_begin(ctx, K_SHADOW, ss)) return e;
                     if(ctx->counting)
-                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], shs, sc_sh,
-                                           cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW));
+                        hipLaunchKernelGGL((k_wf_walk<true, true>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss,
+                                           sc_sh, cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], cnt_for(K_SHADOW),
+                                           ws_for(true));
                     else
-                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], shs, sc_sh,
-                                           cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr);
+                        hipLaunchKernelGGL((k_wf_walk<true, false>), ctx->walk_grid[1], dim3(kBlock), ctx->walk_lds[1], ss,
+                                           sc_sh, cur, counts, r, lists[r & 1], tr, ctx->walk_xcds[1], nullptr, nullptr);
                     PTG_HIP(hipGetLastError());
-                    if(int e = timed_end(ctx, shs)) return e;
-                    if(shs != ss)
-                    {
-                        PTG_HIP(hipEventRecord(sl.ev_shd, shs));
-                        PTG_HIP(hipStreamWaitEvent(ms, sl.ev_shd, 0));
-                    }
+                    if(int e = timed_end(ctx, ss)) return e;
                 }
                 uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
                 // classify/shade need the shadow results, the lists the previous sky
@@ -1161,27 +1115,9 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
                 }
                 if(int e = timed_begin(ctx, K_CLASSIFY, ms)) return e;
-                hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ms, counts, r, tr, cur.meta, hit_list,
-                                   sky_list, lc);
+                hipLaunchKernelGGL(k_wf_classify, grid, dim3(kBlock), 0, ms, counts, r, tr, hit_list, sky_list, lc);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
-                // experiments (PTG_SKY_EARLY): the sky kernel starts right after
-                // classify, beside shade (disjoint sample slots, both only read
-                // this round's state set); the next shadow walk still waits for shade
-                const bool sky_early = overlap && ctx->sky_early;
-                if(sky_early)
-                {
-                    PTG_HIP(hipEventRecord(sl.ev_main, ms));
-                    PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
-                if(int e = timed_begin(ctx, K_SKY, ss)) return e;
-                if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
-                                       cnt_for(K_SHADE));
-                else
-                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
-                PTG_HIP(hipGetLastError());
-                if(int e = timed_end(ctx, ss)) return e;
-                }
                 if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
@@ -1193,15 +1129,13 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 if(int e = timed_end(ctx, ms)) return e;
                 // escaped rays retire without feeding the next round: their
                 // double-precision atmosphere runs on the second stream, overlapping
-                // the next round's latency-bound walks
+                // the next round's latency-bound walks (started beside shade instead,
+                // the two compete for registers: 9% slower on frame 0)
                 if(overlap)
                 {
                     PTG_HIP(hipEventRecord(sl.ev_main, ms));
                     PTG_HIP(hipStreamWaitEvent(sl.side, sl.ev_main, 0));
-                    if(sl.shd) PTG_HIP(hipStreamWaitEvent(sl.shd, sl.ev_main, 0));   // next round's NEE rays
                 }
-                if(!sky_early)
-                {
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
                     hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
@@ -1210,22 +1144,12 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
-                }
             }
             if(overlap)
             {   // join before accumulate
                 PTG_HIP(hipEventRecord(sl.ev_side, sl.side));
                 PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
             }
-        }
-        if(wf && getenv("PTG_DEBUG_QUEUES"))
-        {   // diagnostics: per-round queue sizes of this chunk
-            std::vector<uint32_t> h(2 * (rounds + 2));
-            PTG_HIP(hipMemcpyAsync(h.data(), counts, h.size() * 4, hipMemcpyDeviceToHost, ms));
-            PTG_HIP(hipStreamSynchronize(ms));
-            fprintf(stderr, "chunk j=%u nj=%u lanes=%zu counts:", j, nj, lanes);
-            for(uint32_t v: h) fprintf(stderr, " %u", v);
-            fprintf(stderr, "\n");
         }
         // fold the chunk into the running per-pixel sums, chunks in sample order
         const int first = j == j0, last = j + nj >= j1;
@@ -1267,9 +1191,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
 #endif
     if(ctx->counting)
     {
-        unsigned long long host[K_KINDS * 8];
+        unsigned long long host[kCounterWords];
         PTG_HIP(hipMemcpyAsync(host, ctx->counters.p, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
         PTG_HIP(hipStreamSynchronize(ctx->stream));
+        for(int k = 0; k < 2 * WS_COUNT; ++k) ctx->walk_stats[k / WS_COUNT][k % WS_COUNT] = host[K_KINDS * 8 + k];
         for(int i = 0; i < 8; ++i)
         {
             ctx->last_counters[i] = 0;
@@ -1325,107 +1250,60 @@ int ptg_context_create(int device, ptg_context** out)
         return fail(PTG_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
     std::unique_ptr<ptg_context> ctx(new ptg_context());
     ctx->device = device;
-    const char* cnt = getenv("PTG_COUNTERS");
-    ctx->counting = cnt && cnt[0] == '1';
-    const char* pipe = getenv("PTG_PIPELINE");
-    if(pipe && strcmp(pipe, "megakernel") == 0) ctx->pipeline = 1;
-    if(const char* c = getenv("PTG_CHUNK_LOG2")) ctx->chunk_log2 = uint32_t(std::min(30, std::max(16, atoi(c))));
-    if(const char* c = getenv("PTG_HBM_PCT")) ctx->hbm_pct = uint32_t(std::min(70, std::max(5, atoi(c))));
-    uint32_t per_cu_blocks = 32;   // grid-stride kernels (camera, shade): measured best of 3..128
-    if(const char* w = getenv("PTG_BLOCKS_PER_CU")) per_cu_blocks = uint32_t(std::max(1, atoi(w)));
-    ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * per_cu_blocks;
-    // walk grids: a multiple of what is resident at once (the queue is split
-    // statically over the waves of the whole grid)
+    // grid-stride kernels (camera, classify, shade, sky): 32 blocks per CU,
+    // measured best of 3..128
+    ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 32u;
     // Walk residency: each walk lane holds its world ray (32 B) and its stack
     // window (8 x kCap B) in LDS, so the walk blocks' LDS sets how many are
-    // resident per CU (the LDS may be padded to hold fewer).
-    uint32_t resident[2] = {PTG_WALK_RESIDENT, PTG_WALK_RESIDENT};
-    if(const char* w = getenv("PTG_WALK_RESIDENT")) resident[0] = resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
-    if(const char* w = getenv("PTG_SHADOW_RESIDENT")) resident[1] = uint32_t(std::max(1, std::min(8, atoi(w))));
+    // resident per CU: kWalkResident (the LDS is padded to that share).
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
-    const uint32_t lds_need = kBlock * uint32_t((PTG_WALK_REGCOLD ? 0 : sizeof(WalkCold)) + sizeof(uint2) * LdsStack::kCap);
+    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kCap);
     for(int k = 0; k < 2; ++k)
-        ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / resident[k]) / 1024u * 1024u);
-    int per_cu = 0;
-    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<false, false>, kBlock, ctx->walk_lds[0]) == hipSuccess &&
-       per_cu > 0)
-        ctx->walk_grid[0] = uint32_t(per_cu * prop.multiProcessorCount);
-    if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wf_walk<true, false>, kBlock, ctx->walk_lds[1]) == hipSuccess &&
-       per_cu > 0)
-        ctx->walk_grid[1] = uint32_t(per_cu * prop.multiProcessorCount);
+        ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / kWalkResident) / 1024u * 1024u);
     // One wave of walk blocks, 3 per CU although the LDS holds 4: every block
     // is resident from the start (no oversubscription), and the fourth slot's
     // LDS and registers take the other chunk pipeline's shade and sky waves,
     // which cannot sit beside four walk blocks (their LDS fills the CU).
     // Measured at 1024 spp against the round-1 choice (4 x the resident grid):
     // frame 0 464 vs 495 ms, frame 450 2827 vs 2843, frame 1400 2004 vs 2012
-    // (profiles/r02o_grid/).  PTG_WALK_OVERSUB / PTG_WALK_BLOCKS_PER_CU /
-    // PTG_WALK_GRID / PTG_SHADOW_GRID override it for experiments.
-    uint32_t oversub = 1;
-    if(const char* w = getenv("PTG_WALK_OVERSUB")) oversub = uint32_t(std::max(1, atoi(w)));
-    for(int k = 0; k < 2; ++k) ctx->walk_grid[k] *= oversub;
-    uint32_t walk_per_cu = PTG_WALK_BLOCKS_PER_CU;
-    if(const char* w = getenv("PTG_WALK_BLOCKS_PER_CU")) walk_per_cu = uint32_t(std::max(0, atoi(w)));
-    if(walk_per_cu)
-        for(int k = 0; k < 2; ++k)
-            ctx->walk_grid[k] = std::min(ctx->walk_grid[k], walk_per_cu * uint32_t(prop.multiProcessorCount));
-    const char* gw[2] = {getenv("PTG_WALK_GRID"), getenv("PTG_SHADOW_GRID")};   // experiments: walk grid in blocks
+    // (profiles/r02o_grid/).
+    int per_cu = 0;
+    const void* walks[2] = {reinterpret_cast<const void*>(k_wf_walk<false, false>),
+                            reinterpret_cast<const void*>(k_wf_walk<true, false>)};
     for(int k = 0; k < 2; ++k)
-        if(gw[k]) ctx->walk_grid[k] = uint32_t(std::max(8, atoi(gw[k]))) / 8u * 8u;
-    ctx->walk_grid_r0 = ctx->walk_grid[0];
-    ctx->sky_early = getenv("PTG_SKY_EARLY") != nullptr;
-    if(const char* w = getenv("PTG_WALK_GRID_R0")) ctx->walk_grid_r0 = uint32_t(std::max(8, atoi(w))) / 8u * 8u;
-    for(int k = 0; k < 2; ++k)
-        ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0 && getenv("PTG_NO_XCD") == nullptr) ? 8u : 1u;
+    {
+        per_cu = 0;
+        if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walks[k], kBlock, ctx->walk_lds[k]) != hipSuccess ||
+           per_cu <= 0)
+            per_cu = int(kWalkResident);
+        ctx->walk_grid[k] = std::min<uint32_t>(uint32_t(per_cu), kWalkBlocksPerCu) * uint32_t(prop.multiProcessorCount);
+        ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0) ? 8u : 1u;
+    }
     PTG_HIP(hipSetDevice(device));
 #if PTG_DEBUG
     PTG_HIP(ctx->debug.reserve(kDebugSlots * sizeof(uint32_t)));
     PTG_HIP(hipMemset(ctx->debug.p, 0, kDebugSlots * sizeof(uint32_t)));
 #endif
-    // experiments: PTG_SIDE_PRIO / PTG_MAIN_PRIO = hi | lo give the internal
-    // side (sky, shadow) / extra-slot main streams the device's greatest /
-    // least stream priority
-    auto make_stream = [](hipStream_t* st, const char* env) {
-        const char* v = getenv(env);
-        int least = 0, greatest = 0;
-        if(v && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-            return hipStreamCreateWithPriority(st, hipStreamNonBlocking, v[0] == 'h' ? greatest : least);
-        return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-    };
-    if(getenv("PTG_NO_OVERLAP") == nullptr)
+    PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
+    PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
+    for(uint32_t k = 1; k < kWfSlots; ++k)
     {
-        PTG_HIP(make_stream(&ctx->side, "PTG_SIDE_PRIO"));
-        PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
-        PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
-        uint32_t slots = PTG_WF_SLOTS;
-        if(const char* v = getenv("PTG_SLOTS"))
-            slots = uint32_t(std::max(1, std::min(int(ptg_context::kMaxSlots), atoi(v))));
-        if(slots > 1)
-        {
-            for(uint32_t k = 1; k < slots; ++k)
-            {
-                ptg_context::Slot& b = ctx->slot[k];
-                PTG_HIP(make_stream(&b.main, "PTG_MAIN_PRIO"));
-                PTG_HIP(make_stream(&b.side, "PTG_SIDE_PRIO"));
-                PTG_HIP(hipEventCreateWithFlags(&b.ev_main, hipEventDisableTiming));
-                PTG_HIP(hipEventCreateWithFlags(&b.ev_side, hipEventDisableTiming));
-            }
-            for(uint32_t k = 0; k < slots; ++k)
-            {
-                if(getenv("PTG_SHADOW_STREAM"))
-                {
-                    PTG_HIP(make_stream(&ctx->slot[k].shd, "PTG_SIDE_PRIO"));
-                    PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_shd, hipEventDisableTiming));
-                }
-                PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_done, hipEventDisableTiming));
-                PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_acc, hipEventDisableTiming));
-            }
-            PTG_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
-            PTG_HIP(hipEventCreateWithFlags(&ctx->ev_render_start, hipEventDisableTiming));
-            PTG_HIP(hipEventCreateWithFlags(&ctx->ev_acc_end, hipEventDisableTiming));
-            ctx->nslots = slots;
-        }
+        ptg_context::Slot& b = ctx->slot[k];
+        PTG_HIP(hipStreamCreateWithFlags(&b.main, hipStreamNonBlocking));
+        PTG_HIP(hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking));
+        PTG_HIP(hipEventCreateWithFlags(&b.ev_main, hipEventDisableTiming));
+        PTG_HIP(hipEventCreateWithFlags(&b.ev_side, hipEventDisableTiming));
     }
+    for(uint32_t k = 0; k < kWfSlots; ++k)
+    {
+        PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_done, hipEventDisableTiming));
+        PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_acc, hipEventDisableTiming));
+    }
+    PTG_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
+    PTG_HIP(hipEventCreateWithFlags(&ctx->ev_render_start, hipEventDisableTiming));
+    PTG_HIP(hipEventCreateWithFlags(&ctx->ev_acc_end, hipEventDisableTiming));
+    ctx->nslots = kWfSlots;
     *out = ctx.release();
     return PTG_OK;
 }
@@ -1441,7 +1319,19 @@ void ptg_context_destroy(ptg_context* ctx)
 int ptg_context_set_stream(ptg_context* ctx, void* stream)
 {
     if(int r = bind(ctx)) return r;
-    ctx->stream = static_cast<hipStream_t>(stream);
+    hipStream_t next = static_cast<hipStream_t>(stream);
+    if(next != ctx->stream)
+    {   // work queued on the old stream (a render still reading blocks,
+        // inst_trav, tlas_root) comes before anything queued on the new one,
+        // e.g. the next frame's upload
+        hipEvent_t ev;
+        PTG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, ctx->stream);
+        if(e == hipSuccess) e = hipStreamWaitEvent(next, ev, 0);
+        (void)hipEventDestroy(ev);
+        if(e != hipSuccess) return hip_fail(e, "ptg_context_set_stream: ordering the old stream before the new");
+    }
+    ctx->stream = next;
     return PTG_OK;
 }
 
@@ -1472,8 +1362,8 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     PTG_HIP(ctx->normal.reserve(vertex_count * 16));
     PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
     PTG_HIP(ctx->material.reserve(vertex_count * 16));
-    // 128 bytes of slack: the walk reads a triangle as four (a mixed step:
-    // eight) 16-byte rows
+    // slack: the walk's leaf phase reads a triangle as four 16-byte rows (the
+    // 48-byte record and the next 16 bytes)
     PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 128));
     hipStream_t s = ctx->stream;
     PTG_HIP(hipMemcpyAsync(ctx->indices.p, indices, index_count * 4, hipMemcpyHostToDevice, s));
@@ -1543,17 +1433,8 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     // once and the next render queues right behind the copies.  A staging
     // buffer is reused only after its copies of two uploads ago completed.
     // Growing a device buffer frees the old one, which an in-flight render
-    // may still read: the stream is drained first (rare).
-    bool drained = false;
-    auto grow = [&](DevBuf& b, size_t n) -> hipError_t {
-        if(n <= b.bytes && b.p) return hipSuccess;
-        if(!drained)
-        {
-            if(hipError_t e = hipStreamSynchronize(s)) return e;
-            drained = true;
-        }
-        return b.reserve(n);
-    };
+    // may still read: the context's streams are drained first (rare).
+    auto grow = [&](DevBuf& b, size_t n) { return ctx->grow(b, n); };
     // blocks = [BLAS blocks][TLAS blocks]; growing the buffer drops the BLAS
     // blocks already there, which are then uploaded again
     const std::vector<BlockCopy>& old_blas = ctx->cache.blas;
@@ -1565,7 +1446,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
         ctx->blas_on_device = 0;
     }
     PTG_HIP(grow(ctx->tlas_root, subframe_count * sizeof(uint32_t)));
-    PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav) + 64));   // slack: a mixed walk step reads 8 rows
+    PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav)));
     PTG_HIP(grow(ctx->inst_shade, instance_count * sizeof(InstShade)));
     PTG_HIP(grow(ctx->subframes, subframe_count * sizeof(ptg_subframe)));
     PTG_HIP(grow(ctx->polygon, subframe_count * kPolyStride * sizeof(float2)));
@@ -1733,9 +1614,9 @@ int ptg_path_trace_samples(ptg_context* ctx, const ptg_render_config* cfg, size_
     if(uint64_t(jmax) / cfg->samples_per_motion_blur_step >= ctx->subframe_count)
         return fail(PTG_E_RANGE, "sample index beyond the frame's subframes");
     if(ctx->stack_bound >= PrivStack::kCap) return fail(PTG_E_RANGE, "walk stack bound above the per-sample kernel's stack");
-    PTG_HIP(ctx->tmp_a.reserve(n * sizeof(uint2)));
-    PTG_HIP(ctx->tmp_b.reserve(n * sizeof(int32_t)));
-    PTG_HIP(ctx->tmp_c.reserve(n * sizeof(float4)));
+    PTG_HIP(ctx->grow(ctx->tmp_a, n * sizeof(uint2)));
+    PTG_HIP(ctx->grow(ctx->tmp_b, n * sizeof(int32_t)));
+    PTG_HIP(ctx->grow(ctx->tmp_c, n * sizeof(float4)));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, xy, n * sizeof(uint2), hipMemcpyHostToDevice, ctx->stream));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_b.p, sample_index, n * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_sample_list, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(cfg), uint32_t(n),
@@ -1751,8 +1632,8 @@ int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4*
     if(int r = bind(ctx)) return r;
     if(!n) return PTG_OK;
     if(!color || !out || n >= (1u << 30)) return fail(PTG_E_INVALID, "ptg_tonemap: bad arguments");
-    PTG_HIP(ctx->tmp_c.reserve(n * sizeof(float4)));
-    PTG_HIP(ctx->tmp_a.reserve(n * sizeof(uchar4)));
+    PTG_HIP(ctx->grow(ctx->tmp_c, n * sizeof(float4)));
+    PTG_HIP(ctx->grow(ctx->tmp_a, n * sizeof(uchar4)));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_c.p, color, n * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_tonemap, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, uint32_t(n), ctx->tmp_c.as<float4>(),
                        ctx->tmp_a.as<uchar4>());
@@ -1769,8 +1650,8 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
     if(subframe >= ctx->subframe_count) return fail(PTG_E_RANGE, "subframe out of range");
     if(!n) return PTG_OK;
     if(!rays || !hits || n >= (1u << 28)) return fail(PTG_E_INVALID, "ptg_trace_rays: bad arguments");
-    PTG_HIP(ctx->tmp_a.reserve(n * 32));
-    PTG_HIP(ctx->tmp_b.reserve(n * 32));
+    PTG_HIP(ctx->grow(ctx->tmp_a, n * 32));
+    PTG_HIP(ctx->grow(ctx->tmp_b, n * 32));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, rays, n * 32, hipMemcpyHostToDevice, ctx->stream));
     if(ctx->stack_bound >= PrivStack::kCap) return fail(PTG_E_RANGE, "walk stack bound above the per-ray kernels' stack");
     hipLaunchKernelGGL(k_rays, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, ctx->scene_args(nullptr),
@@ -1784,7 +1665,7 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8])
 {
     if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_counters: bad arguments");
-    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable or PTG_COUNTERS=1)");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable)");
     memcpy(out, ctx->last_counters, sizeof(ctx->last_counters));
     return PTG_OK;
 }
@@ -1842,21 +1723,23 @@ int ptg_last_kernel_busy(ptg_context* ctx, double busy_ms[8], double ms[8], uint
     {
         busy_ms[k] = ms[k] = 0;
         launches[k] = 0;
-        double cs = 0, ce = -1;   // current merged interval of kind k
+        bool open = false;        // a merged interval [cs, ce] of kind k is open
+        double cs = 0, ce = 0;
         for(const Iv& v: iv)
         {
             if(v.kind != k) continue;
             ms[k] += v.e - v.s;
             launches[k] += 1;
-            if(v.s > ce)
+            if(!open || v.s > ce)
             {
-                if(ce > cs) busy_ms[k] += ce - cs;
+                if(open) busy_ms[k] += ce - cs;
                 cs = v.s;
                 ce = v.e;
+                open = true;
             }
             else ce = std::max(ce, v.e);
         }
-        if(ce > cs) busy_ms[k] += ce - cs;
+        if(open) busy_ms[k] += ce - cs;
     }
     ctx->ev_used = 0;
     return PTG_OK;
@@ -1878,8 +1761,24 @@ int ptg_last_timing(ptg_context* ctx, double* trace_ms, uint32_t* launches)
 int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8])
 {
     if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_kernel_counters: bad arguments");
-    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable or PTG_COUNTERS=1)");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable)");
     memcpy(out, ctx->kind_counters, sizeof(ctx->kind_counters));
+    return PTG_OK;
+}
+
+int ptg_last_walk_stats(ptg_context* ctx, uint64_t out[2][8])
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_walk_stats: bad arguments");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable)");
+    static_assert(WS_COUNT == 8, "ptg.h documents 8 walk statistics");
+    memcpy(out, ctx->walk_stats, sizeof(ctx->walk_stats));
+    return PTG_OK;
+}
+
+int ptg_set_hbm_share(ptg_context* ctx, int percent)
+{
+    if(!ctx || percent < 5 || percent > 70) return fail(PTG_E_INVALID, "ptg_set_hbm_share: 5 .. 70 percent");
+    ctx->hbm_pct = uint32_t(percent);
     return PTG_OK;
 }
 

@@ -94,7 +94,7 @@ def assemble_numpy(shard: TileShard, gathered, image):
     return image
 
 
-def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None):
+def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force_collective=True):
     """Render this rank's tiles and gather them into `image` on rank 0.
 
     `renderer` provides render_tiles / scatter_tiles (GpuRenderer, or any
@@ -102,10 +102,15 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None):
     and the scatter - is issued on `stream` (a torch.cuda.Stream; default:
     the current stream), which must be the stream the renderer launches on:
     RCCL then orders the collective after the tiles were written, and the
-    scatter after the collective, with no host synchronisation.  Whenever a
-    process group is initialised the collective runs, at world size 1 too;
-    only a process with no group at all takes the local path.  Over gloo
-    (CPU groups: tests, rehearsals) the tiles go through host memory.
+    scatter after the collective, with no host synchronisation.
+
+    The collective runs when the shard describes this process's place in the
+    default process group (shard.world == group size, shard.rank == group
+    rank; at world size 1 too, with `force_collective`).  A one-rank shard
+    (shard.world == 1) in a larger job, or with no group, is rendered locally;
+    any other mismatch raises before anything is rendered, so no rank waits in
+    a collective the others never join.  Over gloo (CPU groups: tests,
+    rehearsals) the tiles go through host memory.
     """
     import contextlib
 
@@ -113,16 +118,23 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None):
     import torch.distributed as dist
     dev = image.device
     per_tile = shard.tile_w * shard.tile_h
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped and dist.get_world_size() == shard.world and dist.get_rank() == shard.rank:
+        collective = shard.world > 1 or force_collective
+    elif shard.world == 1:
+        collective = False
+    elif not grouped:
+        raise RuntimeError("render_and_gather: world size %d but no process group" % shard.world)
+    else:
+        raise RuntimeError("render_and_gather: shard (rank %d of %d) does not match the process group (rank %d of %d)"
+                           % (shard.rank, shard.world, dist.get_rank(), dist.get_world_size()))
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
     with ctx:
         buf = torch.zeros((shard.max_count * per_tile, 4), dtype=torch.uint8, device=dev)
         if shard.count:
             renderer.render_tiles(cfg, shard.tile_w, shard.tile_h, shard.first, shard.stride, shard.count,
                                   out_bgra=buf[:shard.count * per_tile])
-        grouped = dist.is_available() and dist.is_initialized()
-        if not grouped:
-            if shard.world != 1:
-                raise RuntimeError("render_and_gather: world size %d but no process group" % shard.world)
+        if not collective:
             parts = [buf]
         elif dist.get_backend() == "gloo":   # CPU process groups: gather through host memory
             host = buf.cpu()

@@ -83,6 +83,7 @@ def lib():
     sig = {
         "ptg_abi_version": (I, []),
         "ptg_last_error": (C.c_char_p, []),
+        "ptg_set_host_threads": (I, [I]),
         "ptg_render_config_default": (None, [P]),
         "ptg_scene_load": (I, [C.c_char_p, P, C.POINTER(P)]),
         "ptg_scene_setup_frame": (I, [P, U32]),
@@ -110,6 +111,8 @@ def lib():
         "ptg_last_kernel_times": (I, [P, P, P]),
         "ptg_last_kernel_busy": (I, [P, P, P, P]),
         "ptg_last_kernel_counters": (I, [P, P]),
+        "ptg_last_walk_stats": (I, [P, P]),
+        "ptg_set_hbm_share": (I, [P, I]),
         "ptg_set_pipeline": (I, [P, I]),
         "ptg_set_concurrency": (I, [P, I]),
         "ptg_synchronize": (I, [P]),

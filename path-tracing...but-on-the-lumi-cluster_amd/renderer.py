@@ -174,6 +174,22 @@ class GpuRenderer:
         N.check(N.lib().ptg_last_kernel_counters(self._ctx, out.ctypes.data), "ptg_last_kernel_counters")
         return {k: out[i] for i, k in enumerate(self.KINDS[:6])}
 
+    WALK_STATS = ("node_phases", "node_lanes", "leaf_phases", "leaf_lanes", "refills", "refill_lanes", "iterations",
+                  "active_lanes")
+
+    def walk_stats(self):
+        """{"extend"|"shadow": {stat: count}} of the last counted render: the
+        walks' phases that loaded records and the lanes they served
+        (ptg_last_walk_stats)."""
+        out = np.zeros((2, 8), np.uint64)
+        N.check(N.lib().ptg_last_walk_stats(self._ctx, out.ctypes.data), "ptg_last_walk_stats")
+        return {k: {s: int(out[i, j]) for j, s in enumerate(self.WALK_STATS)} for i, k in enumerate(("extend", "shadow"))}
+
+    def set_hbm_share(self, percent):
+        """Cap the wavefront path state at `percent` of HBM per chunk pipeline
+        (default 35); identical bits at any share."""
+        N.check(N.lib().ptg_set_hbm_share(self._ctx, int(percent)), "ptg_set_hbm_share")
+
     def set_pipeline(self, name):
         """'wavefront' (default) or 'megakernel' - bit-identical results."""
         N.check(N.lib().ptg_set_pipeline(self._ctx, {"wavefront": 0, "megakernel": 1}[name]), "ptg_set_pipeline")

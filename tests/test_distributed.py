@@ -116,3 +116,34 @@ def test_render_and_gather_without_group_is_local():
     assert np.array_equal(image[..., 0].numpy(), xx % 251) and np.array_equal(image[..., 1].numpy(), yy % 241)
     with pytest.raises(RuntimeError, match="no process group"):
         D.render_and_gather(StubRenderer(0), cfg, D.TileShard(cfg, 16, 8, 0, 2), image)
+
+
+def _mismatch_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = N.RenderConfig.make(40, 20, 8)
+    image = torch.zeros((20, 40, 4), dtype=torch.uint8)
+    # a one-rank shard inside a 2-rank job: rendered locally by each rank, no collective
+    D.render_and_gather(StubRenderer(rank), cfg, D.TileShard(cfg, 16, 8, 0, 1), image)
+    yy, xx = np.mgrid[0:20, 0:40]
+    ok = np.array_equal(image[..., 0].numpy(), xx % 251) and (image[..., 2].numpy() == rank).all()
+    # a shard that is not this process's place in the group: refused up front on every rank
+    try:
+        D.render_and_gather(StubRenderer(rank), cfg, D.TileShard(cfg, 16, 8, rank, world + 1), image)
+        refused = False
+    except RuntimeError as e:
+        refused = "does not match the process group" in str(e)
+    np.save(out % rank, np.array([ok, refused]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_render_and_gather_shard_group_mismatch(tmp_path):
+    """distributed.py render_and_gather: a local one-rank shard in a larger job
+    takes the local path (no collective for the other ranks to miss), and a
+    shard that does not describe the process group raises on every rank
+    before anything is rendered."""
+    out = str(tmp_path / "r%d.npy")
+    mp.spawn(_mismatch_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert np.load(out % r).tolist() == [True, True]

@@ -2,7 +2,7 @@
 # Timing-ablation builds (never parity builds): libptg.so variants with extra
 # -D flags, written to <pkg>/_build/ablate_<tag>/libptg.so.  Select one at run
 # time with PTG_LIB=<path> (native.py).
-# Usage: tools/ablate_build.sh <tag> -DPTG_ABLATE_ATMO [...]
+# Usage: tools/ablate_build.sh <tag> <extra hipcc flags, e.g. -fslp-vectorize> [...]
 set -e
 TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
