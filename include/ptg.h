@@ -255,6 +255,18 @@ int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
  * vector-memory instruction of the walk. */
 int ptg_last_walk_stats(ptg_context* ctx, uint64_t out[2][8]);
 
+/* The certified shading of the last ptg_render* call (counting builds, as
+ * ptg_last_counters).  The wavefront pipeline's surface and sky kernels
+ * evaluate the path's double-precision exp / pow / sin / cos with the GPU
+ * library and prove per evaluation that the float the path keeps is the one
+ * glibc's double gives (device/ref_math.h, float_certain); a path with an
+ * evaluation the proof does not cover is shaded again with the restated
+ * glibc algorithms.  out[0] / out[1]: surface / sky paths shaded again;
+ * out[2..8]: per certificate site (acc_exp, exp_times, add_mul_pow,
+ * div_mul_pow, times_cos, times_sin, times_one_minus_div_pow) the paths in
+ * which it failed. */
+int ptg_last_redo_stats(ptg_context* ctx, uint64_t out[9]);
+
 /* Per-launch device timing, measured with HIP events recorded around every
  * kernel launch on the context's stream.  Enabling (re)starts the record;
  * every ptg_render* call after that appends its launches, without blocking

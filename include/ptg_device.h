@@ -39,6 +39,10 @@
 #ifndef PTG_DEVICE_H
 #define PTG_DEVICE_H
 
+#if defined(__FAST_MATH__)
+#error "ptg_device.h: the reference's results need IEEE arithmetic - compile without -ffast-math (see the flags above)"
+#endif
+
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "ptg.h"
@@ -100,12 +104,23 @@ __device__ inline ptg_float3 path_trace_pixel(ptg_uint2 xy, int sample_index, co
                                     link_array, mesh_indices, mesh_pos, mesh_normal, mesh_albedo, mesh_material);
 }
 
+/* The C library's pow, as the reference calls it: glibc's own algorithm on
+ * the device (device/glibc_math.h), glibc itself on the host. */
+__host__ __device__ inline double ptg_libm_pow(double x, double y)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ptg::glibc::pow(x, y);
+#else
+    return pow(x, y);
+#endif
+}
+
 /* tonemap_pixel (path_tracer.hh:753-771): ACES fit, sRGB curve in double as
  * the reference computes it, clamp with glibc's fmin/fmax tie rule, BGRA. */
 __host__ __device__ inline float ptg_tonemap_channel(float c)
 {
     c = (c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f);
-    c = c < 0.0031308f ? c * 12.92f : (float)(pow((double)c, (double)(1.0f / 2.4f)) * (double)1.055f - (double)0.055f);
+    c = c < 0.0031308f ? c * 12.92f : (float)(ptg_libm_pow((double)c, (double)(1.0f / 2.4f)) * (double)1.055f - (double)0.055f);
     c = (c > 0.0f || 0.0f != 0.0f) ? c : 0.0f;                        /* fmax(c, 0): ties -> 0 */
     c = (c < 1.0f || 1.0f != 1.0f) ? c : 1.0f;                        /* fmin(c, 1) */
     return c;

@@ -930,21 +930,21 @@ PTG_D f2 regular_polygon(f2 u, float angle, uint32_t sides, const float2* table 
     if(u.x + u.y > 1.0f) { u.x = 1.0f - u.x; u.y = 1.0f - u.y; }
     return f2{b.x * u.x + c.x * u.y, b.y * u.x + c.y * u.y};
 }
-PTG_D f3 ggx_vndf(f3 view, float roughness, f2 u)                       // :67-83
+template<class MP> PTG_D f3 ggx_vndf(f3 view, float roughness, f2 u, MP& mp)   // :67-83
 {
     if(roughness < 1e-3f) return V3(0, 0, 1);
     const f3 v = normalize(V3(roughness * view.x, roughness * view.y, view.z));
     const float phi = 2.0f * PI_F * u.x;
     const float z = (float)fma((double)(1.0f - u.y), (double)(1.0f + v.z), (double)(-v.z));
     const float sin_theta = fsqrt(clampf(1.0f - z * z, 0.0f, 1.0f));
-    const float x = (float)((double)sin_theta * dcos((double)phi));
-    const float y = (float)((double)sin_theta * dsin((double)phi));
+    const float x = times_cos(sin_theta, (double)phi, mp);
+    const float y = times_sin(sin_theta, (double)phi, mp);
     const f3 h = V3(x, y, z) + v;
     return normalize(V3(roughness * h.x, roughness * h.y, gmax(0.0f, h.z)));
 }
 
 // ---- materials (path_tracer.hh:89-296) ----
-PTG_D float fresnel_att(float vdh, float f0, float eta, float roughness)     // :89-98
+template<class MP> PTG_D float fresnel_att(float vdh, float f0, float eta, float roughness, MP& mp)   // :89-98
 {
     if(eta > 1.0f)
     {
@@ -952,7 +952,7 @@ PTG_D float fresnel_att(float vdh, float f0, float eta, float roughness)     // 
         if(s2 >= 1.0f) return 1.0f;
         vdh = fsqrt(1.0f - s2);
     }
-    return (float)((double)f0 + (double)(gmax(1.0f - roughness, f0) - f0) * dpow((double)gmax(1.0f - vdh, 0.0f), 5.0));
+    return add_mul_pow(f0, gmax(1.0f - roughness, f0) - f0, (double)gmax(1.0f - vdh, 0.0f), 5.0, mp);
 }
 PTG_D float tr_distribution(float hdotn, float a)                            // :105-110
 {
@@ -980,12 +980,13 @@ struct Material {
 };
 
 // bsdf_core (:131-181)
+template<class MP>
 PTG_D f3 bsdf_core(f3 light, f3 h, f3 view, const Material& M, float f0, float distribution, float& rpdf,
-                   float& dpdf, float& tpdf)
+                   float& dpdf, float& tpdf, MP& mp)
 {
     const float ldotn = light.z, vdotn = view.z;
     const float vdoth = dot(view, h), ldoth = dot(light, h);
-    const float fresnel = fresnel_att(vdoth, f0, M.eta, 0);
+    const float fresnel = fresnel_att(vdoth, f0, M.eta, 0, mp);
     const float geometry = tr_masking_shadowing(ldotn, ldoth, vdotn, vdoth, M.roughness);
     const float G1 = tr_masking(vdotn, vdoth, M.roughness);
     f3 color;
@@ -1015,39 +1016,39 @@ PTG_D f3 bsdf_core(f3 light, f3 h, f3 view, const Material& M, float f0, float d
     return color * fabsf(ldotn);
 }
 
-PTG_D void lobe_probs(f3 view, const Material& M, float& f0, float& rp, float& tp, float& dp)
+template<class MP> PTG_D void lobe_probs(f3 view, const Material& M, float& f0, float& rp, float& tp, float& dp, MP& mp)
 {
     float f = (1.0f - M.eta) / (1.0f + M.eta);
     f *= f;
     f0 = f;
     const float lum = dot(M.albedo, V3(0.2126f, 0.7152f, 0.0722f));
-    rp = mixf(1.0f, fresnel_att(view.z, f, M.eta, M.roughness), lum * (1.0f - M.metallic));
+    rp = mixf(1.0f, fresnel_att(view.z, f, M.eta, M.roughness, mp), lum * (1.0f - M.metallic));
     tp = (float)((1.0 - (double)rp) * (double)M.transmission);
     dp = (float)((1.0 - (double)rp) * (double)(1.0f - M.transmission));
 }
 
 // bsdf (:184-222)
-PTG_D f3 bsdf_eval(f3 light, f3 view, const Material& M, float& out_pdf)
+template<class MP> PTG_D f3 bsdf_eval(f3 light, f3 view, const Material& M, float& out_pdf, MP& mp)
 {
     f3 h;
     if(light.z > 0) h = normalize(view + light);
     else h = signf(M.eta - 1.0f) * normalize(light + M.eta * view);
     const float distribution = tr_distribution(h.z, M.roughness);
     float f0, rp, tp, dp;
-    lobe_probs(view, M, f0, rp, tp, dp);
+    lobe_probs(view, M, f0, rp, tp, dp, mp);
     float r, d, t;
-    const f3 att = bsdf_core(light, h, view, M, f0, M.roughness < 1e-3f ? 0.0f : distribution, r, d, t);
+    const f3 att = bsdf_core(light, h, view, M, f0, M.roughness < 1e-3f ? 0.0f : distribution, r, d, t, mp);
     out_pdf = r * rp + d * dp + t * tp;
     return att;
 }
 
 // sample_bsdf (:224-296)
-PTG_D void bsdf_sample(f3 u, f3 view, const Material& M, f3& out_dir, f3& out_att, float& out_pdf)
+template<class MP> PTG_D void bsdf_sample(f3 u, f3 view, const Material& M, f3& out_dir, f3& out_att, float& out_pdf, MP& mp)
 {
     const f2 uxy{u.x, u.y};
-    f3 h = ggx_vndf(view, M.roughness, uxy);
+    f3 h = ggx_vndf(view, M.roughness, uxy, mp);
     float f0, rp, tp, dp;
-    lobe_probs(view, M, f0, rp, tp, dp);
+    lobe_probs(view, M, f0, rp, tp, dp, mp);
     bool diffuse = false, bad;
     if((u.z -= rp) <= 0)
     {   // reflect(-view, h) (math.hh:442-445)
@@ -1085,7 +1086,7 @@ PTG_D void bsdf_sample(f3 u, f3 view, const Material& M, f3& out_dir, f3& out_at
     float distribution = tr_distribution(h.z, M.roughness);
     if(M.roughness < 1e-3f) distribution = diffuse ? 0 : fabsf(4.0f * out_dir.z * view.z);
     float r, d, t;
-    out_att = bsdf_core(out_dir, h, view, M, f0, distribution, r, d, t);
+    out_att = bsdf_core(out_dir, h, view, M, f0, distribution, r, d, t, mp);
     out_pdf = r * rp + t * tp;
     if(M.roughness < 1e-3f && !diffuse) out_pdf = -out_pdf;
     else out_pdf += d * dp;
@@ -1108,7 +1109,7 @@ PTG_D bool ray_sphere(f3 o, f3 d, f3 c, float radius, float& tmin, float& tmax)
 constexpr float RAY_R = 5.8e-6f, RAY_G = 13.6e-6f, RAY_B = 33.1e-6f, MIE_K = 4.0e-6f;
 
 // nishita_atmosphere_attenuation (:456-497)
-PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
+template<class MP> PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax, MP& mp)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     float tmin = 0, atmax = 0;
@@ -1122,8 +1123,8 @@ PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
     {
         const float t = segment * (jitter + (float)i);
         const float height = length((pos + t * view) - earth) - EARTH_RADIUS;
-        ray_depth = (float)((double)ray_depth + dexp((double)ray_h(height)));
-        mie_depth = (float)((double)mie_depth + dexp((double)mie_h(height)));
+        ray_depth = acc_exp(ray_depth, (double)ray_h(height), mp);
+        mie_depth = acc_exp(mie_depth, (double)mie_h(height), mp);
         if(height < 0) shadowed = true;
     }
     if(shadowed) return V3(0.0f, 0.0f, 0.0f);
@@ -1133,7 +1134,9 @@ PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax)
 }
 
 // nishita_atmosphere_scattering (:499-588)
-PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, float tmax, f3& attenuation, f3& in_scatter)
+template<class MP>
+PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, float tmax, f3& attenuation, f3& in_scatter,
+                                 MP& mp)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     attenuation = V3(1.0f, 1.0f, 1.0f);
@@ -1148,8 +1151,8 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
     const float mu = dot(view, L.dir);
     const float rayleigh_phase = 3.0f / (16.0f * PI_F) * (1.0f + mu * mu);
     const float g = MIE_ANISOTROPY;
-    const float mie_phase = (float)((double)(3.0f / (8.0f * PI_F) * (1.0f - g * g) * (1.0f + mu * mu)) /
-                                    ((double)(2.0f + g * g) * dpow((double)(1.0f + g * g - 2.0f * g * mu), 1.5)));
+    const float mie_phase = div_mul_pow((double)(3.0f / (8.0f * PI_F) * (1.0f - g * g) * (1.0f + mu * mu)),
+                                        (double)(2.0f + g * g), (double)(1.0f + g * g - 2.0f * g * mu), 1.5, mp);
     float ray_depth = 0, mie_depth = 0;
     f3 ray_sum = V3(0, 0, 0), mie_sum = V3(0, 0, 0);
     for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
@@ -1164,19 +1167,20 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
         {
             const float tt = light_segment * (jitter.y + (float)j);
             const float height = length((p + tt * L.dir) - earth) - EARTH_RADIUS;
-            lray = (float)((double)lray + dexp((double)ray_h(height)));
-            lmie = (float)((double)lmie + dexp((double)mie_h(height)));
+            lray = acc_exp(lray, (double)ray_h(height), mp);
+            lmie = acc_exp(lmie, (double)mie_h(height), mp);
             if(height < 0) shadowed = true;
         }
         const float height = gmax(length(p - earth) - EARTH_RADIUS, 0.0f);
-        const float ray_density = (float)(dexp((double)ray_h(height)) * (double)segment);
-        const float mie_density = (float)(dexp((double)mie_h(height)) * (double)segment);
+        const float ray_density = exp_times((double)ray_h(height), segment, mp);
+        const float mie_density = exp_times((double)mie_h(height), segment, mp);
         ray_depth += ray_density;
         mie_depth += mie_density;
         const float kr = lray * light_segment + ray_depth, km = lmie * light_segment + mie_depth;
         f3 local = V3(0.0f, 0.0f, 0.0f);
         if(!shadowed)
-            local = V3(fexp(-(RAY_R * kr + MIE_K * km)), fexp(-(RAY_G * kr + MIE_K * km)), fexp(-(RAY_B * kr + MIE_K * km)));
+            local = V3(fexp(-(RAY_R * kr + MIE_K * km)), fexp(-(RAY_G * kr + MIE_K * km)),
+                       fexp(-(RAY_B * kr + MIE_K * km)));
         ray_sum = ray_sum + local * ray_density;
         mie_sum = mie_sum + local * mie_density;
     }
@@ -1198,35 +1202,36 @@ struct NeeCandidate {
     float mis_pdf, jitter;
 };
 
-PTG_D bool nee_prepare(u4& seed, const Light& L, const HitInfo& info, const Material& M, f3 tview, NeeCandidate& c)
+template<class MP>
+PTG_D bool nee_prepare(u4& seed, const Light& L, const HitInfo& info, const Material& M, f3 tview, NeeCandidate& c, MP& mp)
 {
     const f4 u = uniform4(seed);
     c.dir = sample_cone(L.dir, L.cos, f2{u.x, u.y});
     c.jitter = u.w;
     const float nee_pdf = 1.0f / (2.0f * PI_F * (1.0f - L.cos));
     float bsdf_pdf = 0;
-    const f3 b = bsdf_eval(mul_v3m3(c.dir, info.tbn), tview, M, bsdf_pdf);
+    const f3 b = bsdf_eval(mul_v3m3(c.dir, info.tbn), tview, M, bsdf_pdf, mp);
     c.color = (b * nee_pdf) * L.color;
     c.mis_pdf = 1.0f;
     if(L.cos < 1.0f) c.mis_pdf = (nee_pdf * nee_pdf + bsdf_pdf * bsdf_pdf) / nee_pdf;
     return !(c.color.x == 0 && c.color.y == 0 && c.color.z == 0);
 }
 
-PTG_D f3 nee_finish(const NeeCandidate& c, f3 pos)
+template<class MP> PTG_D f3 nee_finish(const NeeCandidate& c, f3 pos, MP& mp)
 {
-    const f3 color = c.color * atmosphere_attenuation(c.jitter, pos, c.dir, MAX_RAY_DIST);
+    const f3 color = c.color * atmosphere_attenuation(c.jitter, pos, c.dir, MAX_RAY_DIST, mp);
     return color / c.mis_pdf;
 }
 
 template<bool COUNT, class SC>
 PTG_D f3 nee_branch(const SC& sc, uint32_t tc, uint32_t to, u4& seed, const Light& L, const HitInfo& info,
-                    const Material& M, f3 tview, Counters& cnt)
+                    const Material& M, f3 tview, Counters& cnt, MathExact& mx)
 {
     NeeCandidate c;
-    if(!nee_prepare(seed, L, info, M, tview, c)) return V3(0, 0, 0);
+    if(!nee_prepare(seed, L, info, M, tview, c, mx)) return V3(0, 0, 0);
     Hit unused;
     if(trace<true, COUNT>(sc, tc, to, info.pos, c.dir, MIN_RAY_DIST, MAX_RAY_DIST, unused, cnt)) return V3(0, 0, 0);
-    return nee_finish(c, info.pos);
+    return nee_finish(c, info.pos, mx);
 }
 
 PTG_D float rd_f(const uint8_t* p, uint32_t off) { return *reinterpret_cast<const float*>(p + off); }
@@ -1299,19 +1304,19 @@ PTG_D f3 tangent_view(f3 ray_dir, const HitInfo& info)
 
 // After tracing bounce ray `ray_dir` from `ray_o` (path_tracer.hh:722-737):
 // MIS, throughput, atmosphere, contribution, path-space regularisation.
+template<class MP>
 PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& info, f3 batt, float bpdf,
-                       f3& attenuation, f3& contribution, float& regularization)
+                       f3& attenuation, f3& contribution, float& regularization, MP& mp)
 {
     const float mis_pdf = bpdf < 0 ? -bpdf : (info.nee_pdf * info.nee_pdf + bpdf * bpdf) / bpdf;
     attenuation = attenuation * batt;
     f3 aatt, insc;
-    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc);
+    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc, mp);
     const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
     contribution = contribution + term / mis_pdf;
     attenuation = attenuation * (aatt / fabsf(bpdf));
     if(bpdf > 0.0f)
-        regularization = (float)((double)regularization *
-                                 gmax_d(1.0 - (double)REGULARIZATION_GAMMA / dpow((double)bpdf, 0.25), 0.0));
+        regularization = times_one_minus_div_pow(regularization, (double)REGULARIZATION_GAMMA, (double)bpdf, 0.25, mp);
     info.roughness = 1.0f - (1.0f - info.roughness) * regularization;
 }
 
@@ -1343,9 +1348,10 @@ PTG_D f3 path_trace_sample(const SC& sc, uint32_t px, uint32_t py, int32_t sampl
     f3 ray_o, ray_dir;
     camera_ray(sc, sf, px, py, sample_index, seed, ray_o, ray_dir);
 
+    MathExact mx;   // glibc's double library algorithms throughout
     HitInfo info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, 0.0f, cnt);
     f3 attenuation, in_scatter;
-    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, attenuation, in_scatter);
+    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, attenuation, in_scatter, mx);
     f3 contribution = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
 
     float regularization = 1.0f;
@@ -1353,15 +1359,15 @@ PTG_D f3 path_trace_sample(const SC& sc, uint32_t px, uint32_t py, int32_t sampl
     {
         const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
         const f3 view = tangent_view(ray_dir, info);
-        contribution = contribution + attenuation * nee_branch<COUNT>(sc, tc, to, seed, L, info, M, view, cnt);
+        contribution = contribution + attenuation * nee_branch<COUNT>(sc, tc, to, seed, L, info, M, view, cnt, mx);
         const f4 ub = uniform4(seed);
         f3 tdir, batt;
         float bpdf;
-        bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf);
+        bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf, mx);
         ray_dir = normalize(mul_m3v3(info.tbn, tdir));
         ray_o = info.pos;
         info = trace_ray<COUNT>(sc, tc, to, L, ray_o, ray_dir, MIN_RAY_DIST, cnt);
-        bounce_tail(seed, L, ray_o, ray_dir, info, batt, bpdf, attenuation, contribution, regularization);
+        bounce_tail(seed, L, ray_o, ray_dir, info, batt, bpdf, attenuation, contribution, regularization, mx);
     }
     return contribution;
 }

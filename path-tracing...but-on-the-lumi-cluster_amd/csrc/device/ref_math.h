@@ -17,6 +17,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "glibc_math.h"
 
 namespace ptg {
 namespace dm {
@@ -121,16 +122,152 @@ PTG_D float signf(float v)
     return v == -0.0f ? -0.0f : +0.0f;
 }
 
-// double-precision library calls, as the reference makes them
-PTG_D double dexp(double x) { return exp(x); }
+// double-precision library calls, as the reference makes them.  exp, pow,
+// sin and cos are glibc's own algorithms (glibc_math.h) wherever their
+// double feeds further double arithmetic: ocml's differ from glibc's on
+// 0.3-25% of float arguments.  log and sqrt, and exp / sin / cos where the
+// path rounds the result straight to float (fexp / fsin / fcos), stay ocml's:
+// over all 2^32 float arguments that float is glibc's
+// (profiles/r03_exhaustive/), and ocml's are table-free and faster.
+PTG_D double dexp(double x) { return glibc::exp(x); }
 PTG_D double dlog(double x) { return log(x); }
-PTG_D double dpow(double x, double y) { return pow(x, y); }
-PTG_D double dsin(double x) { return sin(x); }
-PTG_D double dcos(double x) { return cos(x); }
+PTG_D double dpow(double x, double y) { return glibc::pow(x, y); }
+PTG_D double dsin(double x) { return glibc::sin(x); }
+PTG_D double dcos(double x) { return glibc::cos(x); }
 PTG_D double dsqrt(double x) { return sqrt(x); }
-PTG_D float fcos(float x) { return (float)dcos((double)x); }
-PTG_D float fsin(float x) { return (float)dsin((double)x); }
-PTG_D float fexp(float x) { return (float)dexp((double)x); }
+PTG_D float fcos(float x) { return (float)cos((double)x); }
+PTG_D float fsin(float x) { return (float)sin((double)x); }
+PTG_D float fexp(float x) { return (float)exp((double)x); }
+
+// ---- glibc's float results: exactly, or through ocml plus a certificate --
+// Where the path rounds an expression of a glibc double to float, the two
+// hot shading kernels (k_wf_shade, k_wf_sky) evaluate it with ocml's exp /
+// pow / sin / cos - table-free, and 30-90 fewer VGPRs per kernel than glibc's
+// algorithms inline, which is one more wave per SIMD - and keep that float
+// when it is provably the float glibc's double gives.  When the proof fails
+// (about 1 evaluation in 4 million) the kernel shades that path again with
+// glibc's algorithms (a second, tiny launch over the paths it listed), so
+// every float is glibc's.  The policy type says which: MathExact (glibc's
+// algorithms, glibc_math.h) everywhere else, MathFast in those two kernels.
+//  * D: over every float argument, ocml's double is at most D ulps from
+//    glibc's (tools/exhaustive_f64.hip "distance" rows, profiles/r03_exhaustive/:
+//    exp, sin, cos, pow(x, 5 / 1.5 / 0.25) all 1); kMaxLibDist = 4 is the
+//    largest D the bounds below are sized for.
+//  * each wrapper states how far its double v can then be from the double
+//    the same expression gives with glibc's value: K ulps of v, K <= 4 (D + 1)
+//    (a relative error eps is at most eps 2^53 ulps; two values on either side
+//    of a binade edge count twice).  times_one_minus_div_pow sizes its own
+//    margin.
+//  * float_certain(v): every double within K ulps of v rounds to the same
+//    float as v.  |v| >= 2^128 (inf included): float inf, as for every
+//    double that close; |v| < 2^-151 (zero included): float +-0 (the
+//    wrappers' zero results carry the same sign either way); otherwise v is
+//    more than kCertUlps = 32 > K double ulps away from every float rounding
+//    boundary - the midpoint of two adjacent floats, where the q bits of v
+//    below float's quantum at v equal 2^(q-1) (q = 29 in float's normal
+//    range, 30..54 in its subnormal range, where the quantum is 2^-149).
+//    Across a binade edge v sits next to a float, not a midpoint.  NaN: no
+//    certificate.
+constexpr uint32_t kMaxLibDist = 4;
+constexpr uint32_t kCertUlps = 32;
+PTG_D bool float_certain(double v, uint32_t margin = kCertUlps)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t e = uint32_t(u >> 52) & 0x7ffu;
+    if(e >= 1023u + 128u) return e != 0x7ffu || (u << 12) == 0;             // float inf (not NaN)
+    if(e < 1023u - 151u) return true;                                        // float +-0
+    const uint32_t q = e >= 1023u - 126u ? 29u : 926u - e;                   // bits below float's quantum
+    const uint64_t sig = (u & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    const uint64_t low = sig & ((1ull << q) - 1), mid = 1ull << (q - 1);
+    return (low > mid ? low - mid : mid - low) > margin;
+}
+// the certificate sites (tools/cert_probe.hip counts failures per site)
+enum CertSite { CS_ACC_EXP, CS_EXP_TIMES, CS_ADD_MUL_POW, CS_DIV_MUL_POW, CS_TIMES_COS, CS_TIMES_SIN,
+                CS_TIMES_ONE_MINUS_DIV_POW, CS_COUNT };
+struct MathExact {   // glibc's algorithms
+    static constexpr bool kFast = false;
+    static constexpr uint32_t fail_mask = 0;
+    PTG_D void check(bool, double, int) {}
+};
+struct MathFast {    // ocml's, certified; fail_mask: bit CS_x when a certificate at site x did not hold
+    static constexpr bool kFast = true;
+    uint32_t fail_mask = 0;
+    PTG_D void check(bool certain, double, int site) { fail_mask |= certain ? 0u : 1u << site; }
+};
+
+// (float)((double)acc + exp(x)), acc >= 0: the sum is at least exp(x), so
+// D ulps of exp(x) plus the two roundings is <= 2 (D + 1) ulps of the sum
+// (the factor 2: the two sums may lie in adjacent binades).
+template<class MP> PTG_D float acc_exp(float acc, double x, MP& mp)
+{
+    if(!MP::kFast) return (float)((double)acc + glibc::exp(x));
+    const double v = (double)acc + exp(x);
+    mp.check(acc >= 0.0f && float_certain(v), v, CS_ACC_EXP);
+    return (float)v;
+}
+// (float)(exp(x) * (double)s): D ulps of exp(x) times s is <= 2 D ulps of the
+// product, plus the two roundings: <= 2 (2 D + 1).
+template<class MP> PTG_D float exp_times(double x, float s, MP& mp)
+{
+    if(!MP::kFast) return (float)(glibc::exp(x) * (double)s);
+    const double v = exp(x) * (double)s;
+    mp.check(float_certain(v), v, CS_EXP_TIMES);
+    return (float)v;
+}
+// (float)((double)a + (double)b * pow(x, y)), a, b >= 0: the product is off by
+// <= 2 D + 1 ulps of itself, the sum (>= the product) by one rounding more:
+// <= 2 (2 D + 2) ulps of the sum.
+template<class MP> PTG_D float add_mul_pow(float a, float b, double x, double y, MP& mp)
+{
+    if(!MP::kFast) return (float)((double)a + (double)b * glibc::pow(x, y));
+    const double v = (double)a + (double)b * pow(x, y);
+    mp.check(a >= 0.0f && b >= 0.0f && float_certain(v), v, CS_ADD_MUL_POW);
+    return (float)v;
+}
+// (float)(a / (b * pow(x, y))), b * pow > 0: the divisor's relative error is
+// (D + 1/2) 2^-52, the quotient's (D + 1) 2^-52: <= 4 (D + 1) ulps.
+template<class MP> PTG_D float div_mul_pow(double a, double b, double x, double y, MP& mp)
+{
+    if(!MP::kFast) return (float)(a / (b * glibc::pow(x, y)));
+    const double v = a / (b * pow(x, y));
+    mp.check(float_certain(v), v, CS_DIV_MUL_POW);
+    return (float)v;
+}
+// (float)((double)s * cos(phi)), (float)((double)s * sin(phi)): <= 2 (2 D + 1).
+template<class MP> PTG_D float times_cos(float s, double phi, MP& mp)
+{
+    if(!MP::kFast) return (float)((double)s * glibc::cos(phi));
+    const double v = (double)s * cos(phi);
+    mp.check(float_certain(v), v, CS_TIMES_COS);
+    return (float)v;
+}
+template<class MP> PTG_D float times_sin(float s, double phi, MP& mp)
+{
+    if(!MP::kFast) return (float)((double)s * glibc::sin(phi));
+    const double v = (double)s * sin(phi);
+    mp.check(float_certain(v), v, CS_TIMES_SIN);
+    return (float)v;
+}
+// (float)((double)r * max(1 - g / pow(x, y), 0)), r >= 0.  q = g / pow is off
+// by <= 2 D + 1 ulps of q.  q > 1 + 2^-48: both q exceed 1, the result is
+// r * 0.  Otherwise w = 1 - q (exact for q in [0.5, 1], Sterbenz) is off by
+// (2 D + 1) 2^s + 1 ulps of w, s = exponent of q minus exponent of w (s <= 0
+// when q < 0.5); the product's relative error adds a rounding: the result is
+// off by <= 4 ((2 D + 1) 2^max(s, 0) + 1) + 2 ulps, the margin below.
+template<class MP> PTG_D float times_one_minus_div_pow(float r, double g, double x, double y, MP& mp)
+{
+    if(!MP::kFast) return (float)((double)r * gmax_d(1.0 - g / glibc::pow(x, y), 0.0));
+    const double q = g / pow(x, y);
+    const double w = gmax_d(1.0 - q, 0.0);
+    const double v = (double)r * w;
+    const int32_t s = int32_t((uint64_t)__double_as_longlong(q) >> 52 & 0x7ff) -
+                      int32_t((uint64_t)__double_as_longlong(w) >> 52 & 0x7ff);
+    const bool zero = q > 1.0 + 0x1p-48;
+    const bool small = s <= 16 && w > 0.0;
+    const uint32_t margin = 4u * (((2u * kMaxLibDist + 1u) << (s > 0 ? s : 0)) + 1u) + 2u;
+    mp.check(r >= 0.0f && (zero || (small && float_certain(v, margin))), v, CS_TIMES_ONE_MINUS_DIV_POW);
+    return (float)v;
+}
 
 PTG_D f3 mul_v3m3(f3 b, const m3& a) { return V3(dot(a.r[0], b), dot(a.r[1], b), dot(a.r[2], b)); }
 PTG_D f3 mul_m3v3(const m3& b, f3 a)

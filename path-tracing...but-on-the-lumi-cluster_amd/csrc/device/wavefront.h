@@ -154,16 +154,19 @@ PTG_D u4 to_u4(uint4 v) { return u4{v.x, v.y, v.z, v.w}; }
 PTG_D uint4 to_uint4(u4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
 // Shade one queued path after its current ray was traced (and its pending
-// NEE ray, if any, tested).  Returns true when the path continues; `next` is
-// then the state for the next round.
+// NEE ray, if any, tested).  Returns SH_CONTINUE when the path continues (p
+// is then its state for the next round), SH_DONE when it retired (its sample
+// written), SH_REDO (MathFast only) when a rounding certificate failed:
+// nothing was written and the path must be shaded again with MathExact.
 //
 // KIND as in hit_info: the sky kernel instantiates KIND = 2 (the path's ray
 // missed, so the path ends here), the surface kernel KIND = 1.
-template<bool COUNT, int KIND = 0>
-PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occluded, float4* out_samples,
-                      Counters& cnt)
+enum ShadeResult { SH_DONE = 0, SH_CONTINUE = 1, SH_REDO = 2 };
+template<bool COUNT, int KIND = 0, class MP = MathExact>
+PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occluded, float4* out_samples,
+                             Counters& cnt, MP& mp)
 {
-    if(p.meta.y & META_DEAD) return false;
+    if(p.meta.y & META_DEAD) return SH_DONE;
     const uint8_t* sf = sc.subframes + size_t(meta_sub(p.meta)) * SF_STRIDE;
     const Light L = light_of(sf);
     const uint32_t round = meta_round(p.meta);
@@ -172,7 +175,7 @@ PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occlude
     if(round == 0)
     {   // primary ray (path_tracer.hh:686-693)
         f3 attenuation, in_scatter;
-        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter);
+        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter, mp);
         p.att = attenuation;
         p.contrib = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
         p.reg = 1.0f;
@@ -180,30 +183,32 @@ PTG_D bool shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool occlude
     else
     {   // end of bounce round-1: its NEE term, then the bounce ray's tail
         f3 nee = V3(0, 0, 0);
-        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o);
+        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o, mp);
         p.contrib = p.contrib + p.att * nee;
-        bounce_tail(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg);
+        bounce_tail(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg, mp);
     }
     if(KIND == 2 || !(round < sc.max_bounces && info.thit > 0))
     {
+        if(MP::kFast && mp.fail_mask) return SH_REDO;
         st_out(out_samples + p.meta.x, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f));
-        return false;
+        return SH_DONE;
     }
     // bounce `round` (path_tracer.hh:699-720): NEE setup, BSDF sample, next ray
     const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
     const f3 view = tangent_view(p.ray_d, info);
-    const bool pending = nee_prepare(seed, L, info, M, view, p.nee);
+    const bool pending = nee_prepare(seed, L, info, M, view, p.nee, mp);
     const f4 ub = uniform4(seed);
     f3 tdir, batt;
     float bpdf;
-    bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf);
+    bsdf_sample(V3(ub.x, ub.y, ub.z), view, M, tdir, batt, bpdf, mp);
     p.ray_d = normalize(mul_m3v3(info.tbn, tdir));
     p.ray_o = info.pos;
     p.batt = batt;
     p.bpdf = bpdf;
     p.seed = to_uint4(seed);
     p.meta.y = meta_pack(round + 1, pending, meta_sub(p.meta));
-    return true;
+    if(MP::kFast && mp.fail_mask) return SH_REDO;
+    return SH_CONTINUE;
 }
 
 } // namespace dm

@@ -144,6 +144,17 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
             if(v[k]) atomicAdd(dev + k, v[k]);
 }
 
+// Counting builds: paths the MathFast shading passes listed for the exact
+// pass - [0] surface, [1] sky - then per certificate site (ref_math.h
+// CertSite) the listed paths in which it failed (kRedoWords words).
+constexpr int kRedoWords = 2 + CS_COUNT;
+__device__ __forceinline__ void tally_redo(unsigned long long* tally, int kind, uint32_t fail_mask)
+{
+    atomicAdd(tally + kind, 1ull);
+    for(int k = 0; k < CS_COUNT; ++k)
+        if(fail_mask & (1u << k)) atomicAdd(tally + 2 + k, 1ull);
+}
+
 // ---- wavefront pipeline (csrc/device/wavefront.h) ----
 
 // Lane -> (pixel, sample) of a chunk: a wave holds 8 pixels x 8 consecutive
@@ -216,6 +227,10 @@ constexpr uint32_t kWalkResident = 4;      // walk blocks the LDS holds per CU (
 constexpr uint32_t kWalkBlocksPerCu = 3;   // walk grid: blocks per CU (one resident wave, see ptg_context_create)
 constexpr uint32_t kWfSlots = 2;           // concurrent wavefront chunk pipelines (ptg_context::Slot)
 constexpr uint32_t kBands = 1024;   // XCD bands of a walk queue: a multiple of the XCD count (8 on MI355X)
+// a chunk's device counters: per round the queue / NEE list lengths (2 words,
+// plus 4 spare), the hit / sky list lengths (2), the redo list lengths (2)
+constexpr uint32_t kCountWords(uint32_t rounds) { return 4 * (rounds + 2) + 2 * rounds; }
+constexpr uint32_t kRedoGrid = 16;   // blocks of the MathExact shading passes (grid-stride over a short list)
 
 // Walk statistics of the counting build (per walk kind, see WalkStats): how
 // many lanes each vector-memory instruction of the walk serves.  The walk's
@@ -456,11 +471,16 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
 // next bounce or retire.  Survivors are appended per block (one atomic per
 // queue per block), stored contiguously and grouped by the octant of their
 // next ray, so the next round's 64-ray groups mostly walk one link order.
-template<bool COUNT>
+// MP = MathFast: ocml's double library with rounding certificates (ref_math.h);
+// a path whose certificate failed is listed in redo_list (its length in
+// redo_count) and shaded again by the MathExact instance, which takes
+// redo_list as its hit_list (and appends nothing to a redo list).
+template<bool COUNT, class MP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(
     DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
     const uint32_t* __restrict__ hit_list, const uint32_t* __restrict__ lcounts, uint32_t* __restrict__ next_list,
-    uint32_t* __restrict__ next_shadow, float4* __restrict__ out, unsigned long long* __restrict__ counters)
+    uint32_t* __restrict__ next_shadow, float4* __restrict__ out, uint32_t* __restrict__ redo_list,
+    uint32_t* __restrict__ redo_count, unsigned long long* __restrict__ counters, unsigned long long* __restrict__ redo_tally)
 {
     const uint32_t n = lcounts[0];
     Counters cnt;
@@ -480,8 +500,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
         {
             Hit h;
             bool occluded;
-            load_queued(cur, tr, hit_list[i], p, h, occluded, round > 0);
-            cont = shade_path<COUNT, 1>(sc, p, h, occluded, out, cnt);
+            const uint32_t q = hit_list[i];
+            load_queued(cur, tr, q, p, h, occluded, round > 0);
+            MP mp;
+            const ShadeResult res = shade_path<COUNT, 1, MP>(sc, p, h, occluded, out, cnt, mp);
+            if(MP::kFast && res == SH_REDO)
+            {
+                redo_list[atomicAdd(redo_count, 1u)] = q;
+                if(COUNT) tally_redo(redo_tally, 0, mp.fail_mask);
+            }
+            cont = res == SH_CONTINUE;
             nee = cont && meta_nee(p.meta);
         }
         if(threadIdx.x < 8) oct_count[threadIdx.x] = 0;
@@ -517,11 +545,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 // (path_tracer.hh:456-588), retire.  No survivors.
 #define PTG_SKY_WAVES 5     // 96 VGPRs, no spills (at 8 waves / 64 VGPRs it spilled 49): fits beside 4 walk waves per SIMD
 #define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
-template<bool COUNT>
+// MP and the redo list as in k_wf_shade (the list length in redo_count[1]; the
+// MathExact instance reads its length from lcounts[1]).
+template<bool COUNT, class MP>
 __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr, uint32_t round,
                                                    const uint32_t* __restrict__ sky_list,
                                                    const uint32_t* __restrict__ lcounts, float4* __restrict__ out,
-                                                   unsigned long long* __restrict__ counters)
+                                                   uint32_t* __restrict__ redo_list, uint32_t* __restrict__ redo_count,
+                                                   unsigned long long* __restrict__ counters,
+                                                   unsigned long long* __restrict__ redo_tally)
 {
     const uint32_t n = lcounts[1];
     Counters cnt;
@@ -537,8 +569,14 @@ __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, Pat
         PathRec p;
         Hit h;
         bool occluded;
-        load_queued<true>(cur, tr, sky_list[i], p, h, occluded, round > 0);
-        shade_path<COUNT, 2>(sc, p, h, occluded, out, cnt);
+        const uint32_t q = sky_list[i];
+        load_queued<true>(cur, tr, q, p, h, occluded, round > 0);
+        MP mp;
+        if(shade_path<COUNT, 2, MP>(sc, p, h, occluded, out, cnt, mp) == SH_REDO && MP::kFast)
+        {
+            redo_list[atomicAdd(redo_count + 1, 1u)] = q;
+            if(COUNT) tally_redo(redo_tally, 1, mp.fail_mask);
+        }
     }
     if(COUNT) flush_counters(cnt, counters, 0);
 }
@@ -770,6 +808,7 @@ struct ptg_context {
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
     uint64_t walk_stats[2][8] = {};        // counting builds: WalkStat tallies of the closest-hit / any-hit walks
+    uint64_t redo_stats[kRedoWords] = {};  // counting builds: the certified shading's redo tallies (tally_redo)
     // second stream for the sky kernels + the events that order it with `stream`
     hipStream_t side = nullptr;
     hipEvent_t ev_main = nullptr, ev_side = nullptr;
@@ -903,7 +942,9 @@ enum Kind : int { K_MEGA = 0, K_EXTEND = 1, K_SHADOW = 2, K_SHADE = 3, K_CAMERA 
                   K_SKY = 6, K_CLASSIFY = 7 };
 // counting builds: 8 work counters per kind, then WS_COUNT walk statistics
 // for the closest-hit and the any-hit walk
-constexpr int kCounterWords = K_KINDS * 8 + 2 * WS_COUNT;
+// counting builds' device counters: 8 per kernel kind, the walk statistics,
+// then the certified shading's redo tallies (kRedoWords, tally_redo)
+constexpr int kCounterWords = K_KINDS * 8 + 2 * WS_COUNT + kRedoWords;
 
 int timed_begin(ptg_context* ctx, int kind, hipStream_t st = nullptr);
 int timed_end(ptg_context* ctx, hipStream_t st = nullptr);
@@ -979,13 +1020,14 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         TraceOut trs[2] = {};   // per round parity: the sky kernel of round r reads its set while round r+1 writes the other
         uint32_t* lists[2] = {nullptr, nullptr};
         uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
+        uint32_t *redo_hit = nullptr, *redo_sky = nullptr;   // paths to shade again with MathExact
         uint32_t* counts = nullptr;
     } st[ptg_context::kMaxSlots];
     if(wf)
         for(uint32_t k = 0; k < nslots; ++k)
         {
             const size_t rec = M * 16;
-            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 4 * M * 4 + 4 * (rounds + 2) * 4 + 256));
+            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 6 * M * 4 + kCountWords(rounds) * 4 + 256));
             char* b = slots[k].state->as<char>();
             SlotState& t = st[k];
             for(int h = 0; h < 2; ++h)
@@ -1010,6 +1052,8 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             t.lists[1] = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.sky_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.redo_hit = reinterpret_cast<uint32_t*>(b); b += M * 4;
+            t.redo_sky = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.counts = reinterpret_cast<uint32_t*>(b);
         }
     if(nslots > 1)
@@ -1033,6 +1077,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     const bool overlap = wf && ctx->side != nullptr && ctx->concurrency >= 1;
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
     auto ws_for = [&](bool any) { return cnt_dev ? cnt_dev + 8 * K_KINDS + (any ? WS_COUNT : 0) : nullptr; };
+    unsigned long long* const redo_tally = cnt_dev ? cnt_dev + 8 * K_KINDS + 2 * WS_COUNT : nullptr;
     uint32_t chunk_index = 0;
     for(uint32_t j = j0; j < j1; j += chunk, ++chunk_index)
     {
@@ -1065,7 +1110,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         }
         else
         {
-            PTG_HIP(hipMemsetAsync(counts, 0, 4 * (rounds + 2) * sizeof(uint32_t), ms));
+            PTG_HIP(hipMemsetAsync(counts, 0, kCountWords(rounds) * sizeof(uint32_t), ms));
             const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(persistent, grid_for(lanes))));
             if(int r = timed_begin(ctx, K_CAMERA, ms)) return r;
             if(ctx->counting)
@@ -1107,6 +1152,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                     if(int e = timed_end(ctx, ss)) return e;
                 }
                 uint32_t* lc = counts + 2 * (rounds + 2) + 2 * r;   // this round's hit / sky list lengths
+                uint32_t* rc = counts + 4 * (rounds + 2) + 2 * r;   // this round's redo list lengths (hit, sky)
                 // classify/shade need the shadow results, the lists the previous sky
                 // kernel read, and the state set it read
                 if(overlap)
@@ -1119,12 +1165,25 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
                 if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
+                // the certified pass, then the exact pass over the paths it listed
                 if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_shade<true>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
-                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, cnt_for(K_SHADE));
+                {
+                    hipLaunchKernelGGL((k_wf_shade<true, MathFast>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
+                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, sst.redo_hit, rc,
+                                       cnt_for(K_SHADE), redo_tally);
+                    hipLaunchKernelGGL((k_wf_shade<true, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur, nxt,
+                                       counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out,
+                                       nullptr, nullptr, cnt_for(K_SHADE), nullptr);
+                }
                 else
-                    hipLaunchKernelGGL(k_wf_shade<false>, grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
-                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, nullptr);
+                {
+                    hipLaunchKernelGGL((k_wf_shade<false, MathFast>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
+                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, sst.redo_hit, rc,
+                                       nullptr, nullptr);
+                    hipLaunchKernelGGL((k_wf_shade<false, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur, nxt,
+                                       counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out,
+                                       nullptr, nullptr, nullptr, nullptr);
+                }
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
                 // escaped rays retire without feeding the next round: their
@@ -1138,10 +1197,19 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
-                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
-                                       cnt_for(K_SHADE));
+                {
+                    hipLaunchKernelGGL((k_wf_sky<true, MathFast>), grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc,
+                                       out, sst.redo_sky, rc, cnt_for(K_SHADE), redo_tally);
+                    hipLaunchKernelGGL((k_wf_sky<true, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ss, sc, cur, tr, r,
+                                       sst.redo_sky, rc, out, nullptr, nullptr, cnt_for(K_SHADE), nullptr);
+                }
                 else
-                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
+                {
+                    hipLaunchKernelGGL((k_wf_sky<false, MathFast>), grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc,
+                                       out, sst.redo_sky, rc, nullptr, nullptr);
+                    hipLaunchKernelGGL((k_wf_sky<false, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ss, sc, cur, tr, r,
+                                       sst.redo_sky, rc, out, nullptr, nullptr, nullptr, nullptr);
+                }
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
             }
@@ -1195,6 +1263,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipMemcpyAsync(host, ctx->counters.p, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
         PTG_HIP(hipStreamSynchronize(ctx->stream));
         for(int k = 0; k < 2 * WS_COUNT; ++k) ctx->walk_stats[k / WS_COUNT][k % WS_COUNT] = host[K_KINDS * 8 + k];
+        for(int k = 0; k < kRedoWords; ++k) ctx->redo_stats[k] = host[K_KINDS * 8 + 2 * WS_COUNT + k];
         for(int i = 0; i < 8; ++i)
         {
             ctx->last_counters[i] = 0;
@@ -1763,6 +1832,15 @@ int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8])
     if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_kernel_counters: bad arguments");
     if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable)");
     memcpy(out, ctx->kind_counters, sizeof(ctx->kind_counters));
+    return PTG_OK;
+}
+
+int ptg_last_redo_stats(ptg_context* ctx, uint64_t out[9])
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_last_redo_stats: bad arguments");
+    if(!ctx->counting) return fail(PTG_E_INVALID, "counters disabled (ptg_counters_enable)");
+    static_assert(kRedoWords == 9, "ptg.h documents 9 words");
+    memcpy(out, ctx->redo_stats, sizeof(ctx->redo_stats));
     return PTG_OK;
 }
 

@@ -194,6 +194,16 @@ class GpuRenderer:
         """'wavefront' (default) or 'megakernel' - bit-identical results."""
         N.check(N.lib().ptg_set_pipeline(self._ctx, {"wavefront": 0, "megakernel": 1}[name]), "ptg_set_pipeline")
 
+    def redo_stats(self):
+        """Counting renders: paths the certified shading passes handed to the
+        exact (glibc-algorithm) pass - {"surface", "sky", "sites": {site: n}}
+        (ptg_last_redo_stats)."""
+        out = np.zeros(9, np.uint64)
+        N.check(N.lib().ptg_last_redo_stats(self._ctx, out.ctypes.data), "ptg_last_redo_stats")
+        names = ("acc_exp", "exp_times", "add_mul_pow", "div_mul_pow", "times_cos", "times_sin",
+                 "times_one_minus_div_pow")
+        return {"surface": int(out[0]), "sky": int(out[1]), "sites": {n: int(out[2 + k]) for k, n in enumerate(names)}}
+
     def set_concurrency(self, level):
         """0: one stream; 1: sky/shadow kernels on a second stream; 2 (default):
         also two sample chunks in flight.  Identical bits at every level."""

@@ -37,6 +37,8 @@ if a.counters:
     kc = r.kernel_counters()
     names = ["samples", "visits", "tri_tests", "blas_entries", "queries", "shades", "tlas_visits", "wave_iters"]
     extra = {k: {n: int(v[i]) for i, n in enumerate(names)} for k, v in kc.items() if int(v[:8].sum())}
+    if a.pipeline == "wavefront":
+        extra["redo"] = r.redo_stats()
 print(json.dumps({"counters": extra, "lib": os.path.basename(N.LIB_PATH), "pipeline": a.pipeline, "spp": a.spp, "bounces": a.bounces,
                   "frame": a.frame, "wall_ms": round(best, 2), "msamples_per_s": round(a.width * a.height * a.spp / best / 1e3, 2),
                   "kernels_ms": {k: round(v[0], 2) for k, v in kt.items() if v[1]}}))

@@ -16,7 +16,9 @@
 // product's own device function, the host evaluates glibc's (the library the
 // reference and the oracle link), and the two doubles must be the same bits
 // (any NaN matches any NaN):
-//   exp(x) log(x) sin(x) cos(x) sqrt(x)               all x
+//   exp(x) log(x) sqrt(x)                              all x
+//   sin(x) cos(x)        |x| < 105414350 (glibc_math.h's domain; the path: [0, 2 pi])
+//   (float)sin(x), (float)cos(x), (float)exp(x)   fsin / fcos / fexp, ocml, all x, float result
 //   pow(x, 5.0)                                       fresnel_att (:91-98)
 //   pow(x, 0.25)                                      path-space regularisation (:735-737)
 //   pow(x, 1.5)                                       Mie phase (:531)
@@ -37,12 +39,25 @@
 
 using namespace ptg::dm;
 
-enum Fn { F_EXP, F_LOG, F_SIN, F_COS, F_SQRT, F_POW5, F_POW025, F_POW15, F_POWSRGB, F_INVERF, F_COUNT };
-static const char* kNames[F_COUNT] = {"exp(x)", "log(x)", "sin(x)", "cos(x)", "sqrt(x)", "pow(x, 5.0)",
-                                      "pow(x, 0.25)", "pow(x, 1.5)", "pow(x, (double)(1.0f / 2.4f))",
-                                      "inv_erf(x), |x| <= 1 - 1e-6"};
-
+enum Fn { F_EXP, F_LOG, F_SIN, F_COS, F_SQRT, F_POW5, F_POW025, F_POW15, F_POWSRGB, F_INVERF, F_FSIN, F_FCOS, F_FEXP, F_DEXP, F_DSIN, F_DCOS, F_DPOW5, F_DPOW15, F_DPOW025, F_COUNT };
+// F_D*: "distance" rows - ocml's double (the certified shading, ref_math.h) against glibc's: the
+// largest distance in ulps over all float arguments, which must not exceed kMaxLibDist
+static bool is_distance(int fn) { return fn >= F_DEXP; }
+static const char* kNames[F_COUNT] = {"exp(x)", "log(x)", "sin(x), |x| < 105414350", "cos(x), |x| < 105414350",
+                                      "sqrt(x)", "pow(x, 5.0)", "pow(x, 0.25)", "pow(x, 1.5)",
+                                      "pow(x, (double)(1.0f / 2.4f))", "inv_erf(x), |x| <= 1 - 1e-6",
+                                      "(float)sin(x) (fsin)", "(float)cos(x) (fcos)", "(float)exp(x) (fexp)",
+                                      "distance ocml exp(x)", "distance ocml sin(x)", "distance ocml cos(x)",
+                                      "distance ocml pow(x, 5.0)", "distance ocml pow(x, 1.5)", "distance ocml pow(x, 0.25)"};
 constexpr float kErfLimit = 1.0f - 1e-6f;   // sample_gaussian's clamp (path_tracer.hh:12-17)
+constexpr float kSinCosLimit = 105414350.0f;   // glibc's reduce_sincos range (s_sin.c)
+static __host__ __device__ bool in_domain(int fn, float x)
+{
+    if(fn == F_INVERF) return x >= -kErfLimit && x <= kErfLimit;
+    if(fn == F_SIN || fn == F_COS) return fabsf(x) < kSinCosLimit;
+    return true;
+}
+
 
 __global__ void k_eval(int fn, uint64_t begin, uint32_t n, uint64_t* __restrict__ out)
 {
@@ -62,6 +77,15 @@ __global__ void k_eval(int fn, uint64_t begin, uint32_t n, uint64_t* __restrict_
         case F_POW025: r = dpow(d, 0.25); break;
         case F_POW15: r = dpow(d, 1.5); break;
         case F_POWSRGB: r = dpow(d, (double)(1.0f / 2.4f)); break;
+        case F_FSIN: r = (double)fsin(x); break;
+        case F_FCOS: r = (double)fcos(x); break;
+        case F_FEXP: r = (double)fexp(x); break;
+        case F_DEXP: r = exp(d); break;
+        case F_DSIN: r = sin(d); break;
+        case F_DCOS: r = cos(d); break;
+        case F_DPOW5: r = pow(d, 5.0); break;
+        case F_DPOW15: r = pow(d, 1.5); break;
+        case F_DPOW025: r = pow(d, 0.25); break;
         default: r = (x >= -kErfLimit && x <= kErfLimit) ? (double)ptg::dm::inv_erf(x) : 0.0; break;
         }
         out[i] = __double_as_longlong(r);
@@ -100,6 +124,15 @@ static double host_eval(int fn, float x)
     case F_POW025: return pow(d, 0.25);
     case F_POW15: return pow(d, 1.5);
     case F_POWSRGB: return pow(d, (double)(1.0f / 2.4f));
+    case F_FSIN: return (double)(float)sin(d);
+    case F_FCOS: return (double)(float)cos(d);
+    case F_FEXP: return (double)(float)exp(d);
+    case F_DEXP: return exp(d);
+    case F_DSIN: return sin(d);
+    case F_DCOS: return cos(d);
+    case F_DPOW5: return pow(d, 5.0);
+    case F_DPOW15: return pow(d, 1.5);
+    case F_DPOW025: return pow(d, 0.25);
     default: return (x >= -kErfLimit && x <= kErfLimit) ? (double)host_inv_erf(x) : 0.0;
     }
 }
@@ -109,6 +142,16 @@ static uint64_t bits(double v)
     uint64_t u;
     memcpy(&u, &v, 8);
     return u;
+}
+// distance in ulps of two doubles (as adjacent doubles count 1); NaN vs number
+// or opposite signs (zeros aside): "infinite"
+static uint64_t ulp_distance(double a, double b)
+{
+    if(a != a || b != b) return (a != a && b != b) ? 0 : ~0ull;
+    if(a == 0 && b == 0) return 0;
+    const int64_t ia = int64_t(bits(a) & 0x7fffffffffffffffull), ib = int64_t(bits(b) & 0x7fffffffffffffffull);
+    if((bits(a) >> 63) != (bits(b) >> 63)) return ~0ull;
+    return uint64_t(ia > ib ? ia - ib : ib - ia);
 }
 
 int main(int argc, char** argv)
@@ -130,6 +173,8 @@ int main(int argc, char** argv)
         const auto t0 = std::chrono::steady_clock::now();
         std::atomic<uint64_t> mismatch{0}, float_mismatch{0}, domain{0};
         std::mutex mu;
+        uint64_t max_dist = 0;   // distance rows: largest |ulp distance|, at max_x
+        uint32_t max_x = 0;
         std::vector<uint32_t> examples;
         for(uint64_t b = 0; b < (1ull << 32); b += chunk)
         {
@@ -142,19 +187,25 @@ int main(int argc, char** argv)
             std::vector<std::thread> pool;
             for(int t = 0; t < threads; ++t)
                 pool.emplace_back([&, t] {
-                    uint64_t mis = 0, fmis = 0, dom = 0;
+                    uint64_t mis = 0, fmis = 0, dom = 0, dmax = 0;
+                    uint32_t dx = 0;
                     for(uint32_t i = uint32_t(uint64_t(chunk) * t / threads); i < uint32_t(uint64_t(chunk) * (t + 1) / threads); ++i)
                     {
                         const uint32_t u = uint32_t(b + i);
                         float x;
                         memcpy(&x, &u, 4);
-                        if(fn == F_INVERF && !(x >= -kErfLimit && x <= kErfLimit)) continue;
+                        if(!in_domain(fn, x)) continue;
                         ++dom;
                         const double want = host_eval(fn, x);
                         double got;
                         memcpy(&got, &host[i], 8);
                         if(bits(want) == bits(got) || (want != want && got != got)) continue;
                         ++mis;
+                        if(is_distance(fn))
+                        {
+                            const uint64_t dd = ulp_distance(want, got);
+                            if(dd > dmax) { dmax = dd; dx = u; }
+                        }
                         const float fw = (float)want, fg = (float)got;
                         uint32_t uw, ug;
                         memcpy(&uw, &fw, 4);
@@ -166,6 +217,8 @@ int main(int argc, char** argv)
                     mismatch += mis;
                     float_mismatch += fmis;
                     domain += dom;
+                    std::lock_guard<std::mutex> g(mu);
+                    if(dmax > max_dist) { max_dist = dmax; max_x = dx; }
                 });
             for(std::thread& th: pool) th.join();
             if((b / chunk) % 16 == 15)
@@ -179,7 +232,7 @@ int main(int argc, char** argv)
         printf("%s over %llu float inputs: %llu double mismatches (%llu of them also after rounding to float), %.1f s\n",
                kNames[fn], (unsigned long long)domain.load(), (unsigned long long)mismatch.load(),
                (unsigned long long)float_mismatch.load(), secs);
-        for(uint32_t u: examples)
+        for(uint32_t u: is_distance(fn) ? std::vector<uint32_t>() : examples)
         {
             float x;
             memcpy(&x, &u, 4);
@@ -192,8 +245,18 @@ int main(int argc, char** argv)
             printf("  x = 0x%08x (%.9g): glibc %.17g (0x%016llx), device %.17g (0x%016llx)\n", u, d, want,
                    (unsigned long long)bits(want), got, (unsigned long long)bits(got));
         }
+        if(is_distance(fn))
+        {   // the bound the certified shading relies on (ref_math.h kMaxLibDist)
+            float x;
+            memcpy(&x, &max_x, 4);
+            printf("%s: largest distance %llu ulps (x = 0x%08x, %.9g); bound kMaxLibDist = %u: %s\n", kNames[fn],
+                   (unsigned long long)max_dist, max_x, (double)x, ptg::dm::kMaxLibDist,
+                   max_dist <= ptg::dm::kMaxLibDist ? "holds" : "VIOLATED");
+            if(max_dist > ptg::dm::kMaxLibDist) status = 1;
+        }
+        else if(mismatch.load())
+            status = 1;
         fflush(stdout);
-        if(mismatch.load()) status = 1;
     }
     return status;
 }

@@ -22,13 +22,31 @@ run() {   # run <name> <seconds> <cmd...>: output to gpurun_out/<name>.txt
 for step in ${STEPS:-tests smoke}; do
   case $step in
     probe) run pk_probe 120 tools/_bin/pk_probe; rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    hazard) run pk_hazard 120 tools/_bin/pk_hazard; rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    anim) run gpu_anim 900 python -u -m pytest tests/test_gpu_animation.py -m gpu -x -v -s --timeout 880 --timeout-method thread || exit $? ;;
+    slptri) run slp_tri_noslp 120 tools/_bin/slp_tri_noslp gpurun_out/slp_tri_noslp.bin || exit $?
+            run slp_tri_slp 120 tools/_bin/slp_tri_slp gpurun_out/slp_tri_slp.bin || exit $?
+            python3 tools/slp_tri_cmp.py gpurun_out/slp_tri_noslp.bin gpurun_out/slp_tri_slp.bin | tee gpurun_out/slp_tri_cmp.txt; rm -f gpurun_out/slp_tri_*.bin ;;
     slp) PTG_LIB=$P/ablate_slp/libptg.so run slp_rays 200 python tools/rays_diff.py || exit $? ;;
+    slpvar) for v in ${SLPV:-slp}; do
+              PTG_LIB=$P/ablate_$v/libptg.so run slp_rays_$v 200 python tools/rays_diff.py || exit $?
+            done ;;
     slpbisect) for d in $P/ablate_slpT*; do
                  PTG_LIB=$d/libptg.so run slp_rays_$(basename $d) 200 python tools/rays_diff.py || exit $?
                done ;;
     tests) run gpu_tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     exf64) run exhaustive_f64 1100 tools/exhaustive_f64.sh; rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    exf64bin) for fn in ${FNS:-0 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17 18}; do
+                run exhaustive_f64_$fn 600 tools/_bin/exhaustive_f64 $fn; rc=$?; [ $rc -le 1 ] || exit $rc
+              done ;;
+    parity) run gpu_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_dropin.py -m gpu -x -q --timeout 500 --timeout-method thread || exit $? ;;
+    ab) for lib in ${LIBS:-default}; do
+          for f in ${FRAMES:-0 450}; do
+            if [ "$lib" = default ]; then L=""; else L=$P/ablate_$lib/libptg.so; fi
+            PTG_LIB=$L run ab_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} || exit $?
+          done
+        done ;;
     bench) run bench 1100 python bench.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
