@@ -45,6 +45,7 @@
 
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <string.h>
 #include "ptg.h"
 #include "device/path_tracer.h"
 
@@ -134,6 +135,97 @@ __host__ __device__ inline ptg_uchar4 tonemap_pixel(ptg_float3 color)
     o.z = (uint8_t)roundf(ptg_tonemap_channel(color.x) * 255.0f);
     o.w = 255;
     return o;
+}
+
+/* ---- ptg_device_selftest: known answers in the including translation unit -
+ * The results above are the reference's bits only under the compile flags
+ * named at the top of this header.  -ffast-math is refused at compile time;
+ * the others leave no macro to test, so this self-test runs known-answer
+ * checks compiled with the caller's own flags, on the caller's device, and
+ * returns a bit mask of the checks that failed (0: all passed; negative: a
+ * HIP error code, negated):
+ *   bit 0  float a * b + c was contracted into an fma (-ffp-contract=off missing)
+ *   bit 1  exp, bit 2 pow, bit 3 sin / cos: the device's glibc restatements
+ *          against this host's libm on arguments where other libraries differ
+ *   bit 4  tonemap_pixel on the device against the host's
+ *   bit 5  fmin's tie rule (glibc: equal operands give the second)
+ *   bit 6  float division and reciprocal, correctly rounded (the walk's
+ *          reciprocals and -fhip-fp32-correctly-rounded-divide-sqrt)
+ * The SLP vectoriser's divergence shows only inside a
+ * whole BVH walk; tests/test_gpu_parity.py's ray records catch it. */
+namespace ptg_selftest {
+enum { kArgs = 8 };
+struct Io {
+    float a, b, c, fma_out;         /* contraction probe */
+    float x[kArgs];                 /* library arguments */
+    double exp_out[kArgs], pow_out[kArgs], sin_out[kArgs], cos_out[kArgs];
+    ptg_float3 colors[kArgs];
+    ptg_uchar4 tone_out[kArgs];
+    float tie_out[2];
+    float div_out[kArgs], rcp_out[kArgs];
+};
+__global__ void kernel(Io* io)
+{
+    if(threadIdx.x != 0 || blockIdx.x != 0) return;
+    io->fma_out = io->a * io->b + io->c;
+    for(int i = 0; i < kArgs; ++i)
+    {
+        const double d = (double)io->x[i];
+        io->exp_out[i] = ptg::glibc::exp(d);
+        io->pow_out[i] = ptg::glibc::pow(d, (double)(1.0f / 2.4f));
+        io->sin_out[i] = ptg::glibc::sin(d);
+        io->cos_out[i] = ptg::glibc::cos(d);
+        io->tone_out[i] = tonemap_pixel(io->colors[i]);
+        io->div_out[i] = io->a / io->x[i];
+        io->rcp_out[i] = ptg::dm::rcp_rn(io->x[i]);
+    }
+    io->tie_out[0] = ptg::dm::gmin(io->c - io->c, -(io->c - io->c));   /* fmin(+0, -0): -0 */
+    io->tie_out[1] = ptg::dm::gmax(-(io->c - io->c), io->c - io->c);   /* fmax(-0, +0): +0 */
+}
+inline bool same(double a, double b) { return memcmp(&a, &b, sizeof a) == 0; }
+inline bool samef(float a, float b) { return memcmp(&a, &b, sizeof a) == 0; }
+} // namespace ptg_selftest
+
+static inline int ptg_device_selftest(hipStream_t stream = nullptr)
+{
+    using namespace ptg_selftest;
+    Io h;
+    memset(&h, 0, sizeof h);
+    h.a = 1.0f + 0x1p-12f; h.b = 1.0f + 0x1p-12f; h.c = -(1.0f + 0x1p-11f);   /* fused: 2^-24, unfused: 0 */
+    /* arguments where ocml's double differs from glibc's (profiles/r03_exhaustive) */
+    const float xs[kArgs] = {0x1.58a68ap-24f, 0.00591448275f, 0.0040609352f, 1.7f, 3.0f, 0.7531f, 5.25f, 0x1.fffffep-1f};
+    for(int i = 0; i < kArgs; ++i)
+    {
+        h.x[i] = xs[i];
+        h.colors[i].x = xs[i] * 0.5f; h.colors[i].y = xs[i]; h.colors[i].z = xs[i] * 2.0f;
+    }
+    Io* d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(Io));
+    if(e == hipSuccess) e = hipMemcpyAsync(d, &h, sizeof(Io), hipMemcpyHostToDevice, stream);
+    if(e == hipSuccess)
+    {
+        hipLaunchKernelGGL(ptg_selftest::kernel, dim3(1), dim3(64), 0, stream, d);
+        e = hipGetLastError();
+    }
+    Io r;
+    if(e == hipSuccess) e = hipMemcpyAsync(&r, d, sizeof(Io), hipMemcpyDeviceToHost, stream);
+    if(e == hipSuccess) e = hipStreamSynchronize(stream);
+    if(d) (void)hipFree(d);
+    if(e != hipSuccess) return -(int)e;
+    int bad = 0;
+    if(r.fma_out != 0.0f) bad |= 1;
+    for(int i = 0; i < kArgs; ++i)
+    {
+        const double x = (double)h.x[i];
+        if(!same(r.exp_out[i], exp(x))) bad |= 2;
+        if(!same(r.pow_out[i], pow(x, (double)(1.0f / 2.4f)))) bad |= 4;
+        if(!same(r.sin_out[i], sin(x)) || !same(r.cos_out[i], cos(x))) bad |= 8;
+        const ptg_uchar4 t = tonemap_pixel(h.colors[i]);
+        if(memcmp(&t, &r.tone_out[i], sizeof t) != 0) bad |= 16;
+        if(!samef(r.div_out[i], h.a / h.x[i]) || !samef(r.rcp_out[i], 1.0f / h.x[i])) bad |= 64;
+    }
+    if(!samef(r.tie_out[0], -0.0f) || !samef(r.tie_out[1], 0.0f)) bad |= 32;
+    return bad;
 }
 
 #endif /* PTG_DEVICE_H */

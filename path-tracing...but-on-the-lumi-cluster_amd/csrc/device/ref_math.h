@@ -195,6 +195,13 @@ struct MathFast {    // ocml's, certified; fail_mask: bit CS_x when a certificat
     PTG_D void check(bool certain, double, int site) { fail_mask |= certain ? 0u : 1u << site; }
 };
 
+// Arguments where both libraries return the exact value, so the double is
+// the same whatever follows: exp(0) = 1, sin(0) = 0, cos(0) = 1, pow(1, y) = 1,
+// pow(0, y > 0) = 0 (C99 F.9; the path meets them - pow(1, 0.25) on every
+// rejected BSDF sample, whose pdf is 1 - and their results are often exact
+// float ties, which no rounding certificate covers).
+PTG_D bool pow_exact_arg(double x, double y) { return x == 1.0 || (x == 0.0 && y > 0.0); }
+
 // (float)((double)acc + exp(x)), acc >= 0: the sum is at least exp(x), so
 // D ulps of exp(x) plus the two roundings is <= 2 (D + 1) ulps of the sum
 // (the factor 2: the two sums may lie in adjacent binades).
@@ -202,7 +209,7 @@ template<class MP> PTG_D float acc_exp(float acc, double x, MP& mp)
 {
     if(!MP::kFast) return (float)((double)acc + glibc::exp(x));
     const double v = (double)acc + exp(x);
-    mp.check(acc >= 0.0f && float_certain(v), v, CS_ACC_EXP);
+    mp.check(x == 0.0 || (acc >= 0.0f && float_certain(v)), v, CS_ACC_EXP);
     return (float)v;
 }
 // (float)(exp(x) * (double)s): D ulps of exp(x) times s is <= 2 D ulps of the
@@ -211,7 +218,7 @@ template<class MP> PTG_D float exp_times(double x, float s, MP& mp)
 {
     if(!MP::kFast) return (float)(glibc::exp(x) * (double)s);
     const double v = exp(x) * (double)s;
-    mp.check(float_certain(v), v, CS_EXP_TIMES);
+    mp.check(x == 0.0 || float_certain(v), v, CS_EXP_TIMES);
     return (float)v;
 }
 // (float)((double)a + (double)b * pow(x, y)), a, b >= 0: the product is off by
@@ -221,7 +228,7 @@ template<class MP> PTG_D float add_mul_pow(float a, float b, double x, double y,
 {
     if(!MP::kFast) return (float)((double)a + (double)b * glibc::pow(x, y));
     const double v = (double)a + (double)b * pow(x, y);
-    mp.check(a >= 0.0f && b >= 0.0f && float_certain(v), v, CS_ADD_MUL_POW);
+    mp.check(pow_exact_arg(x, y) || (a >= 0.0f && b >= 0.0f && float_certain(v)), v, CS_ADD_MUL_POW);
     return (float)v;
 }
 // (float)(a / (b * pow(x, y))), b * pow > 0: the divisor's relative error is
@@ -230,7 +237,7 @@ template<class MP> PTG_D float div_mul_pow(double a, double b, double x, double 
 {
     if(!MP::kFast) return (float)(a / (b * glibc::pow(x, y)));
     const double v = a / (b * pow(x, y));
-    mp.check(float_certain(v), v, CS_DIV_MUL_POW);
+    mp.check(pow_exact_arg(x, y) || float_certain(v), v, CS_DIV_MUL_POW);
     return (float)v;
 }
 // (float)((double)s * cos(phi)), (float)((double)s * sin(phi)): <= 2 (2 D + 1).
@@ -238,14 +245,14 @@ template<class MP> PTG_D float times_cos(float s, double phi, MP& mp)
 {
     if(!MP::kFast) return (float)((double)s * glibc::cos(phi));
     const double v = (double)s * cos(phi);
-    mp.check(float_certain(v), v, CS_TIMES_COS);
+    mp.check(phi == 0.0 || float_certain(v), v, CS_TIMES_COS);
     return (float)v;
 }
 template<class MP> PTG_D float times_sin(float s, double phi, MP& mp)
 {
     if(!MP::kFast) return (float)((double)s * glibc::sin(phi));
     const double v = (double)s * sin(phi);
-    mp.check(float_certain(v), v, CS_TIMES_SIN);
+    mp.check(phi == 0.0 || float_certain(v), v, CS_TIMES_SIN);
     return (float)v;
 }
 // (float)((double)r * max(1 - g / pow(x, y), 0)), r >= 0.  q = g / pow is off
@@ -265,7 +272,8 @@ template<class MP> PTG_D float times_one_minus_div_pow(float r, double g, double
     const bool zero = q > 1.0 + 0x1p-48;
     const bool small = s <= 16 && w > 0.0;
     const uint32_t margin = 4u * (((2u * kMaxLibDist + 1u) << (s > 0 ? s : 0)) + 1u) + 2u;
-    mp.check(r >= 0.0f && (zero || (small && float_certain(v, margin))), v, CS_TIMES_ONE_MINUS_DIV_POW);
+    mp.check(pow_exact_arg(x, y) || (r >= 0.0f && (zero || (small && float_certain(v, margin)))), v,
+             CS_TIMES_ONE_MINUS_DIV_POW);
     return (float)v;
 }
 

@@ -40,7 +40,7 @@ using namespace ptg::dm;
 namespace {
 
 constexpr int kBlock = 256;
-#define PTG_SHADE_WAVES 2
+#define PTG_SHADE_WAVES 3   // the certified pass (MathFast): 168 VGPRs, 6 spilled; the exact pass runs at 2
 
 // ---------------------------------------------------------------- kernels --
 
@@ -476,7 +476,7 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
 // redo_count) and shaded again by the MathExact instance, which takes
 // redo_list as its hit_list (and appends nothing to a redo list).
 template<bool COUNT, class MP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHADE_WAVES, 8))) void k_wf_shade(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MP::kFast ? PTG_SHADE_WAVES : 2, 8))) void k_wf_shade(
     DevScene sc, PathSoA cur, PathSoA nxt, uint32_t* __restrict__ counts, uint32_t round, TraceOut tr,
     const uint32_t* __restrict__ hit_list, const uint32_t* __restrict__ lcounts, uint32_t* __restrict__ next_list,
     uint32_t* __restrict__ next_shadow, float4* __restrict__ out, uint32_t* __restrict__ redo_list,
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SHAD
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
 // (path_tracer.hh:456-588), retire.  No survivors.
 #define PTG_SKY_WAVES 5     // 96 VGPRs, no spills (at 8 waves / 64 VGPRs it spilled 49): fits beside 4 walk waves per SIMD
-#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8)))
+#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(MP::kFast ? PTG_SKY_WAVES : 4, 8)))
 // MP and the redo list as in k_wf_shade (the list length in redo_count[1]; the
 // MathExact instance reads its length from lcounts[1]).
 template<bool COUNT, class MP>

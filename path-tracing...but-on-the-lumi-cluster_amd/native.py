@@ -78,6 +78,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise OSError("libptg.so not built at %s - run __graft_entry__.build()" % LIB_PATH)
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64.so.7 and
+    # loads it under a different DT_NEEDED name, so a libptg loaded first would
+    # bring in ROCm's copy beside it, and whichever runtime opens the GPU
+    # second finds no device (hipErrorNoDevice; tools/probe_libs.py).  With
+    # torch imported first, libptg's libamdhip64.so.7 resolves to torch's.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P, U32, SZ, I = C.c_void_p, C.c_uint32, C.c_size_t, C.c_int
     sig = {

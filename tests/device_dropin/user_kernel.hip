@@ -34,6 +34,9 @@ __global__ void k_user_tonemap(uint32_t n, const ptg_float4* __restrict__ in, pt
 
 extern "C" {
 
+// ptg_device_selftest() compiled with this library's flags (ptg_device.h)
+int user_selftest() { return ptg_device_selftest(); }
+
 // All array pointers are DEVICE pointers; synchronous.
 int user_path_trace(const ptg_render_config* cfg, uint32_t n, const ptg_uint2* xy, const int32_t* js,
                     const ptg_subframe* subframes, const ptg_tlas_instance* instances, const ptg_bvh_node* nodes,

@@ -115,3 +115,24 @@ def test_device_tonemap_pixel_matches_reference():
     out = torch.zeros((len(colors), 4), dtype=torch.uint8, device="cuda:0")
     assert _lib().user_tonemap_device(len(colors), C.c_void_p(colors.data_ptr()), C.c_void_p(out.data_ptr())) == 0
     assert np.array_equal(out.cpu().numpy(), g["bgra"])
+
+
+@pytest.mark.gpu
+def test_device_selftest_passes(native_lib):
+    """ptg_device_selftest() (ptg_device.h), compiled with the documented
+    flags in the user's library: every known-answer check passes."""
+    L = _lib()
+    L.user_selftest.restype = C.c_int
+    assert L.user_selftest() == 0
+
+
+@pytest.mark.gpu
+def test_device_selftest_flags_contraction(native_lib):
+    """The same user code built with -ffp-contract=fast: the self-test reports
+    the contraction (bit 0) instead of passing silently."""
+    path = os.path.join(ROOT, "tests", "device_dropin", "_build", "libuser_kernel_contract.so")
+    assert os.path.exists(path), "build it first: __graft_entry__.build() (tests/device_dropin/Makefile)"
+    L = C.CDLL(path)
+    L.user_selftest.restype = C.c_int
+    r = L.user_selftest()
+    assert r > 0 and (r & 1), r

@@ -1,4 +1,4 @@
-# variant: the sky kernel at 4 waves per SIMD (its VGPR cap 128) instead of 5
+# variant: the certified sky pass at 4 waves per SIMD (its VGPR cap 128) instead of 5
 import sys
 p = sys.argv[1] + "/pt_kernels.hip"
 s = open(p).read()
