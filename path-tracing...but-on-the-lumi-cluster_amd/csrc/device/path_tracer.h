@@ -1117,17 +1117,23 @@ template<class MP> PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view
     tmin = (float)gmax_d((double)tmin, 0.0);
     tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
     const float segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
+    // The reference sums the depths over every step and then returns 0 if a
+    // step lay below the ground; the sums are only read when none did, so the
+    // heights are tested first and the exp work is skipped for a shadowed ray
+    // (the same result; the heights are recomputed bit for bit).
+    for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
+    {
+        const float t = segment * (jitter + (float)i);
+        if(length((pos + t * view) - earth) - EARTH_RADIUS < 0) return V3(0.0f, 0.0f, 0.0f);
+    }
     float ray_depth = 0, mie_depth = 0;
-    bool shadowed = false;
     for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
     {
         const float t = segment * (jitter + (float)i);
         const float height = length((pos + t * view) - earth) - EARTH_RADIUS;
         ray_depth = acc_exp(ray_depth, (double)ray_h(height), mp);
         mie_depth = acc_exp(mie_depth, (double)mie_h(height), mp);
-        if(height < 0) shadowed = true;
     }
-    if(shadowed) return V3(0.0f, 0.0f, 0.0f);
     const f3 tau = V3((RAY_R * ray_depth + MIE_K * mie_depth) * segment, (RAY_G * ray_depth + MIE_K * mie_depth) * segment,
                       (RAY_B * ray_depth + MIE_K * mie_depth) * segment);
     return V3(fexp(-tau.x), fexp(-tau.y), fexp(-tau.z));
@@ -1162,15 +1168,20 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
         ray_sphere(p, L.dir, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, tmax);   // keeps old values on a miss
         const float light_segment = (tmax - tmin) / (float)SECONDARY_ITERATIONS;
         float lray = 0, lmie = 0;
-        bool shadowed = false;
+        bool shadowed = false;   // lray / lmie are read only if not (heights tested first, as above)
         for(int j = 0; j < SECONDARY_ITERATIONS; ++j)
         {
             const float tt = light_segment * (jitter.y + (float)j);
-            const float height = length((p + tt * L.dir) - earth) - EARTH_RADIUS;
-            lray = acc_exp(lray, (double)ray_h(height), mp);
-            lmie = acc_exp(lmie, (double)mie_h(height), mp);
-            if(height < 0) shadowed = true;
+            if(length((p + tt * L.dir) - earth) - EARTH_RADIUS < 0) shadowed = true;
         }
+        if(!shadowed)
+            for(int j = 0; j < SECONDARY_ITERATIONS; ++j)
+            {
+                const float tt = light_segment * (jitter.y + (float)j);
+                const float height = length((p + tt * L.dir) - earth) - EARTH_RADIUS;
+                lray = acc_exp(lray, (double)ray_h(height), mp);
+                lmie = acc_exp(lmie, (double)mie_h(height), mp);
+            }
         const float height = gmax(length(p - earth) - EARTH_RADIUS, 0.0f);
         const float ray_density = exp_times((double)ray_h(height), segment, mp);
         const float mie_density = exp_times((double)mie_h(height), segment, mp);
@@ -1304,7 +1315,10 @@ PTG_D f3 tangent_view(f3 ray_dir, const HitInfo& info)
 
 // After tracing bounce ray `ray_dir` from `ray_o` (path_tracer.hh:722-737):
 // MIS, throughput, atmosphere, contribution, path-space regularisation.
-template<class MP>
+// NEED_REG = false: the caller retires the path after this, so the
+// regularised roughness is never read (the certified sky pass would otherwise
+// spend a pow and its certificate on a dead value).
+template<class MP, bool NEED_REG = true>
 PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& info, f3 batt, float bpdf,
                        f3& attenuation, f3& contribution, float& regularization, MP& mp)
 {
@@ -1315,6 +1329,7 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
     const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
     contribution = contribution + term / mis_pdf;
     attenuation = attenuation * (aatt / fabsf(bpdf));
+    if(!NEED_REG) return;
     if(bpdf > 0.0f)
         regularization = times_one_minus_div_pow(regularization, (double)REGULARIZATION_GAMMA, (double)bpdf, 0.25, mp);
     info.roughness = 1.0f - (1.0f - info.roughness) * regularization;

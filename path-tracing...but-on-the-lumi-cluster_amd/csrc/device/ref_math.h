@@ -170,9 +170,10 @@ PTG_D float fexp(float x) { return (float)exp((double)x); }
 //    certificate.
 constexpr uint32_t kMaxLibDist = 4;
 constexpr uint32_t kCertUlps = 32;
-PTG_D bool float_certain(double v, uint32_t margin = kCertUlps)
+// float_certain's rare ranges (float inf / zero / subnormal results), out of
+// the inlined fast path
+__device__ __noinline__ inline bool float_certain_wide(uint64_t u, uint32_t margin)
 {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
     const uint32_t e = uint32_t(u >> 52) & 0x7ffu;
     if(e >= 1023u + 128u) return e != 0x7ffu || (u << 12) == 0;             // float inf (not NaN)
     if(e < 1023u - 151u) return true;                                        // float +-0
@@ -181,16 +182,33 @@ PTG_D bool float_certain(double v, uint32_t margin = kCertUlps)
     const uint64_t low = sig & ((1ull << q) - 1), mid = 1ull << (q - 1);
     return (low > mid ? low - mid : mid - low) > margin;
 }
+PTG_D bool float_certain(double v, uint32_t margin = kCertUlps)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    // float's normal range, exponent 897..1150: the 29 bits below float
+    // precision are in the low word; their distance from 2^28 is > margin
+    if(uint32_t(u >> 52 & 0x7ffu) - (1023u - 126u) <= 253u)
+        return ((uint32_t(u) - (0x10000000u - margin)) & 0x1fffffffu) > 2u * margin;
+    return float_certain_wide(u, margin);
+}
 // the certificate sites (tools/cert_probe.hip counts failures per site)
 enum CertSite { CS_ACC_EXP, CS_EXP_TIMES, CS_ADD_MUL_POW, CS_DIV_MUL_POW, CS_TIMES_COS, CS_TIMES_SIN,
                 CS_TIMES_ONE_MINUS_DIV_POW, CS_COUNT };
-struct MathExact {   // glibc's algorithms
+struct MathExact {   // glibc's algorithms, exp's table in global memory
     static constexpr bool kFast = false;
+    static constexpr bool kLdsExp = false;
     static constexpr uint32_t fail_mask = 0;
     PTG_D void check(bool, double, int) {}
+    PTG_D double exp(double x) const { return glibc::exp(x); }
+};
+struct MathExactLds : MathExact {   // the same, exp's table copied to LDS by the kernel (glibc::exp_table_to_lds)
+    static constexpr bool kLdsExp = true;
+    glibc::ExpTabLds xt;
+    PTG_D double exp(double x) const { return glibc::exp(x, xt); }
 };
 struct MathFast {    // ocml's, certified; fail_mask: bit CS_x when a certificate at site x did not hold
     static constexpr bool kFast = true;
+    static constexpr bool kLdsExp = false;
     uint32_t fail_mask = 0;
     PTG_D void check(bool certain, double, int site) { fail_mask |= certain ? 0u : 1u << site; }
 };
@@ -207,7 +225,7 @@ PTG_D bool pow_exact_arg(double x, double y) { return x == 1.0 || (x == 0.0 && y
 // (the factor 2: the two sums may lie in adjacent binades).
 template<class MP> PTG_D float acc_exp(float acc, double x, MP& mp)
 {
-    if(!MP::kFast) return (float)((double)acc + glibc::exp(x));
+    if constexpr(!MP::kFast) return (float)((double)acc + mp.exp(x));
     const double v = (double)acc + exp(x);
     mp.check(x == 0.0 || (acc >= 0.0f && float_certain(v)), v, CS_ACC_EXP);
     return (float)v;
@@ -216,7 +234,7 @@ template<class MP> PTG_D float acc_exp(float acc, double x, MP& mp)
 // product, plus the two roundings: <= 2 (2 D + 1).
 template<class MP> PTG_D float exp_times(double x, float s, MP& mp)
 {
-    if(!MP::kFast) return (float)(glibc::exp(x) * (double)s);
+    if constexpr(!MP::kFast) return (float)(mp.exp(x) * (double)s);
     const double v = exp(x) * (double)s;
     mp.check(x == 0.0 || float_certain(v), v, CS_EXP_TIMES);
     return (float)v;
@@ -226,7 +244,7 @@ template<class MP> PTG_D float exp_times(double x, float s, MP& mp)
 // <= 2 (2 D + 2) ulps of the sum.
 template<class MP> PTG_D float add_mul_pow(float a, float b, double x, double y, MP& mp)
 {
-    if(!MP::kFast) return (float)((double)a + (double)b * glibc::pow(x, y));
+    if constexpr(!MP::kFast) return (float)((double)a + (double)b * glibc::pow(x, y));
     const double v = (double)a + (double)b * pow(x, y);
     mp.check(pow_exact_arg(x, y) || (a >= 0.0f && b >= 0.0f && float_certain(v)), v, CS_ADD_MUL_POW);
     return (float)v;
@@ -235,7 +253,7 @@ template<class MP> PTG_D float add_mul_pow(float a, float b, double x, double y,
 // (D + 1/2) 2^-52, the quotient's (D + 1) 2^-52: <= 4 (D + 1) ulps.
 template<class MP> PTG_D float div_mul_pow(double a, double b, double x, double y, MP& mp)
 {
-    if(!MP::kFast) return (float)(a / (b * glibc::pow(x, y)));
+    if constexpr(!MP::kFast) return (float)(a / (b * glibc::pow(x, y)));
     const double v = a / (b * pow(x, y));
     mp.check(pow_exact_arg(x, y) || float_certain(v), v, CS_DIV_MUL_POW);
     return (float)v;
@@ -243,14 +261,14 @@ template<class MP> PTG_D float div_mul_pow(double a, double b, double x, double 
 // (float)((double)s * cos(phi)), (float)((double)s * sin(phi)): <= 2 (2 D + 1).
 template<class MP> PTG_D float times_cos(float s, double phi, MP& mp)
 {
-    if(!MP::kFast) return (float)((double)s * glibc::cos(phi));
+    if constexpr(!MP::kFast) return (float)((double)s * glibc::cos(phi));
     const double v = (double)s * cos(phi);
     mp.check(phi == 0.0 || float_certain(v), v, CS_TIMES_COS);
     return (float)v;
 }
 template<class MP> PTG_D float times_sin(float s, double phi, MP& mp)
 {
-    if(!MP::kFast) return (float)((double)s * glibc::sin(phi));
+    if constexpr(!MP::kFast) return (float)((double)s * glibc::sin(phi));
     const double v = (double)s * sin(phi);
     mp.check(phi == 0.0 || float_certain(v), v, CS_TIMES_SIN);
     return (float)v;
@@ -263,7 +281,7 @@ template<class MP> PTG_D float times_sin(float s, double phi, MP& mp)
 // off by <= 4 ((2 D + 1) 2^max(s, 0) + 1) + 2 ulps, the margin below.
 template<class MP> PTG_D float times_one_minus_div_pow(float r, double g, double x, double y, MP& mp)
 {
-    if(!MP::kFast) return (float)((double)r * gmax_d(1.0 - g / glibc::pow(x, y), 0.0));
+    if constexpr(!MP::kFast) return (float)((double)r * gmax_d(1.0 - g / glibc::pow(x, y), 0.0));
     const double q = g / pow(x, y);
     const double w = gmax_d(1.0 - q, 0.0);
     const double v = (double)r * w;

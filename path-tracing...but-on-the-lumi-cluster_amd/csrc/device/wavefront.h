@@ -185,7 +185,7 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
         f3 nee = V3(0, 0, 0);
         if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o, mp);
         p.contrib = p.contrib + p.att * nee;
-        bounce_tail(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg, mp);
+        bounce_tail<MP, KIND != 2>(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg, mp);
     }
     if(KIND == 2 || !(round < sc.max_bounces && info.thit > 0))
     {

@@ -41,6 +41,9 @@ namespace {
 
 constexpr int kBlock = 256;
 #define PTG_SHADE_WAVES 3   // the certified pass (MathFast): 168 VGPRs, 6 spilled; the exact pass runs at 2
+// the surface pass's math: MathFast (certified ocml + the exact redo pass) or
+// MathExactLds (glibc's algorithms directly, no redo)
+using ShadeMath = MathFast;
 
 // ---------------------------------------------------------------- kernels --
 
@@ -467,6 +470,23 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
     h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
 }
 
+// A shading kernel's math policy (ref_math.h); MathExactLds copies glibc
+// exp's table into the kernel's LDS array first (every thread, before any
+// returns).
+template<class MP>
+__device__ __forceinline__ MP shading_policy(glibc::u2v* exp_tab)
+{
+    MP mp;
+    if constexpr(MP::kLdsExp)
+    {
+        glibc::exp_table_to_lds((glibc::lds_u2v_t*)exp_tab);   // C cast: generic -> LDS address space
+        __syncthreads();
+        mp.xt = glibc::ExpTabLds{(const glibc::lds_u2v_t*)exp_tab};
+    }
+    (void)exp_tab;
+    return mp;
+}
+
 // Surface hits: NEE finish, bounce tail, then NEE setup + BSDF sample of the
 // next bounce or retire.  Survivors are appended per block (one atomic per
 // queue per block), stored contiguously and grouped by the octant of their
@@ -485,6 +505,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MP::kFas
     const uint32_t n = lcounts[0];
     Counters cnt;
     __shared__ uint32_t oct_count[8], oct_start[8], blk_base, nee_total, nee_base;
+    __shared__ glibc::u2v exp_tab[MP::kLdsExp ? glibc::kExpTabEntries : 1];
+    const MP mp0 = shading_policy<MP>(exp_tab);
     for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
     {
         const uint32_t i = base + threadIdx.x;
@@ -502,7 +524,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MP::kFas
             bool occluded;
             const uint32_t q = hit_list[i];
             load_queued(cur, tr, q, p, h, occluded, round > 0);
-            MP mp;
+            MP mp = mp0;
             const ShadeResult res = shade_path<COUNT, 1, MP>(sc, p, h, occluded, out, cnt, mp);
             if(MP::kFast && res == SH_REDO)
             {
@@ -542,21 +564,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MP::kFas
 }
 
 // Rays that left the scene: sun disk, NEE finish, the atmosphere integrals
-// (path_tracer.hh:456-588), retire.  No survivors.
-#define PTG_SKY_WAVES 5     // 96 VGPRs, no spills (at 8 waves / 64 VGPRs it spilled 49): fits beside 4 walk waves per SIMD
-#define PTG_SKY_ATTR __attribute__((amdgpu_waves_per_eu(MP::kFast ? PTG_SKY_WAVES : 4, 8)))
-// MP and the redo list as in k_wf_shade (the list length in redo_count[1]; the
-// MathExact instance reads its length from lcounts[1]).
-template<bool COUNT, class MP>
-__global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, PathSoA cur, TraceOut tr, uint32_t round,
-                                                   const uint32_t* __restrict__ sky_list,
-                                                   const uint32_t* __restrict__ lcounts, float4* __restrict__ out,
-                                                   uint32_t* __restrict__ redo_list, uint32_t* __restrict__ redo_count,
-                                                   unsigned long long* __restrict__ counters,
-                                                   unsigned long long* __restrict__ redo_tally)
+// (path_tracer.hh:456-588), retire.  No survivors.  The atmosphere is exp
+// work end to end, and here glibc's restated exp (its table copied to LDS)
+// beats ocml's plus rounding certificates (MathFast: 2x the code, spills at
+// 5 waves; measured DESIGN.md section 4), so this pass is exact by itself.
+#define PTG_SKY_WAVES 4     // 112 VGPRs, no spills
+template<bool COUNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8))) void k_wf_sky(
+    DevScene sc, PathSoA cur, TraceOut tr, uint32_t round, const uint32_t* __restrict__ sky_list,
+    const uint32_t* __restrict__ lcounts, float4* __restrict__ out, unsigned long long* __restrict__ counters)
 {
     const uint32_t n = lcounts[1];
     Counters cnt;
+    __shared__ glibc::u2v exp_tab[glibc::kExpTabEntries];
+    MathExactLds mp = shading_policy<MathExactLds>(exp_tab);
     for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     {
 #if PTG_DEBUG
@@ -569,14 +590,8 @@ __global__ __launch_bounds__(kBlock) PTG_SKY_ATTR void k_wf_sky(DevScene sc, Pat
         PathRec p;
         Hit h;
         bool occluded;
-        const uint32_t q = sky_list[i];
-        load_queued<true>(cur, tr, q, p, h, occluded, round > 0);
-        MP mp;
-        if(shade_path<COUNT, 2, MP>(sc, p, h, occluded, out, cnt, mp) == SH_REDO && MP::kFast)
-        {
-            redo_list[atomicAdd(redo_count + 1, 1u)] = q;
-            if(COUNT) tally_redo(redo_tally, 1, mp.fail_mask);
-        }
+        load_queued<true>(cur, tr, sky_list[i], p, h, occluded, round > 0);
+        shade_path<COUNT, 2>(sc, p, h, occluded, out, cnt, mp);
     }
     if(COUNT) flush_counters(cnt, counters, 0);
 }
@@ -1020,14 +1035,14 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         TraceOut trs[2] = {};   // per round parity: the sky kernel of round r reads its set while round r+1 writes the other
         uint32_t* lists[2] = {nullptr, nullptr};
         uint32_t *hit_list = nullptr, *sky_list = nullptr;   // this round's paths by shading kernel
-        uint32_t *redo_hit = nullptr, *redo_sky = nullptr;   // paths to shade again with MathExact
+        uint32_t* redo_hit = nullptr;   // surface paths to shade again with MathExact
         uint32_t* counts = nullptr;
     } st[ptg_context::kMaxSlots];
     if(wf)
         for(uint32_t k = 0; k < nslots; ++k)
         {
             const size_t rec = M * 16;
-            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 6 * M * 4 + kCountWords(rounds) * 4 + 256));
+            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 5 * M * 4 + kCountWords(rounds) * 4 + 256));
             char* b = slots[k].state->as<char>();
             SlotState& t = st[k];
             for(int h = 0; h < 2; ++h)
@@ -1053,7 +1068,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             t.hit_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.sky_list = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.redo_hit = reinterpret_cast<uint32_t*>(b); b += M * 4;
-            t.redo_sky = reinterpret_cast<uint32_t*>(b); b += M * 4;
             t.counts = reinterpret_cast<uint32_t*>(b);
         }
     if(nslots > 1)
@@ -1167,22 +1181,23 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 if(int e = timed_begin(ctx, K_SHADE, ms)) return e;
                 // the certified pass, then the exact pass over the paths it listed
                 if(ctx->counting)
-                {
-                    hipLaunchKernelGGL((k_wf_shade<true, MathFast>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
+                    hipLaunchKernelGGL((k_wf_shade<true, ShadeMath>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
                                        hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, sst.redo_hit, rc,
                                        cnt_for(K_SHADE), redo_tally);
-                    hipLaunchKernelGGL((k_wf_shade<true, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur, nxt,
-                                       counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out,
-                                       nullptr, nullptr, cnt_for(K_SHADE), nullptr);
-                }
                 else
+                    hipLaunchKernelGGL((k_wf_shade<false, ShadeMath>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r,
+                                       tr, hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, sst.redo_hit,
+                                       rc, nullptr, nullptr);
+                if constexpr(ShadeMath::kFast)
                 {
-                    hipLaunchKernelGGL((k_wf_shade<false, MathFast>), grid, dim3(kBlock), 0, ms, sc, cur, nxt, counts, r, tr,
-                                       hit_list, lc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out, sst.redo_hit, rc,
-                                       nullptr, nullptr);
-                    hipLaunchKernelGGL((k_wf_shade<false, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur, nxt,
-                                       counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1], trs[(r + 1) & 1].shadow, out,
-                                       nullptr, nullptr, nullptr, nullptr);
+                    if(ctx->counting)
+                        hipLaunchKernelGGL((k_wf_shade<true, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur,
+                                           nxt, counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1],
+                                           trs[(r + 1) & 1].shadow, out, nullptr, nullptr, cnt_for(K_SHADE), nullptr);
+                    else
+                        hipLaunchKernelGGL((k_wf_shade<false, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ms, sc, cur,
+                                           nxt, counts, r, tr, sst.redo_hit, rc, lists[(r + 1) & 1],
+                                           trs[(r + 1) & 1].shadow, out, nullptr, nullptr, nullptr, nullptr);
                 }
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ms)) return e;
@@ -1197,19 +1212,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 }
                 if(int e = timed_begin(ctx, K_SKY, ss)) return e;
                 if(ctx->counting)
-                {
-                    hipLaunchKernelGGL((k_wf_sky<true, MathFast>), grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc,
-                                       out, sst.redo_sky, rc, cnt_for(K_SHADE), redo_tally);
-                    hipLaunchKernelGGL((k_wf_sky<true, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ss, sc, cur, tr, r,
-                                       sst.redo_sky, rc, out, nullptr, nullptr, cnt_for(K_SHADE), nullptr);
-                }
+                    hipLaunchKernelGGL(k_wf_sky<true>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out,
+                                       cnt_for(K_SHADE));
                 else
-                {
-                    hipLaunchKernelGGL((k_wf_sky<false, MathFast>), grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc,
-                                       out, sst.redo_sky, rc, nullptr, nullptr);
-                    hipLaunchKernelGGL((k_wf_sky<false, MathExact>), dim3(kRedoGrid), dim3(kBlock), 0, ss, sc, cur, tr, r,
-                                       sst.redo_sky, rc, out, nullptr, nullptr, nullptr, nullptr);
-                }
+                    hipLaunchKernelGGL(k_wf_sky<false>, grid, dim3(kBlock), 0, ss, sc, cur, tr, r, sky_list, lc, out, nullptr);
                 PTG_HIP(hipGetLastError());
                 if(int e = timed_end(ctx, ss)) return e;
             }
