@@ -22,7 +22,8 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-KERNELS = {"extend": "k_wf_walk<false, false>", "shadow": "k_wf_walk<true, false>", "shade": "k_wf_shade<false>",
+KERNELS = {"extend": "k_wf_walk<false, false>", "shadow": "k_wf_walk<true, false>",
+           "shade": "k_wf_shade<false, ptg::dm::MathFast>", "shade_exact": "k_wf_shade<false, ptg::dm::MathExact>",
            "camera": "k_wf_camera<false>", "accumulate": "k_accumulate", "megakernel": "k_trace<false>",
            "sky": "k_wf_sky<false>", "classify": "k_wf_classify"}
 
