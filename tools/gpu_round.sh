@@ -41,10 +41,12 @@ for step in ${STEPS:-tests smoke}; do
                 run exhaustive_f64_$fn 600 tools/_bin/exhaustive_f64 $fn; rc=$?; [ $rc -le 1 ] || exit $rc
               done ;;
     parity) run gpu_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_dropin.py -m gpu -x -q --timeout 500 --timeout-method thread || exit $? ;;
-    ab) for lib in ${LIBS:-default}; do
+    ab) k=0
+        for lib in ${LIBS:-default}; do
+          k=$((k+1))   # run index: a library named twice (interleaved repeats) keeps both outputs
           for f in ${FRAMES:-0 450}; do
             if [ "$lib" = default ]; then L=""; else L=$P/ablate_$lib/libptg.so; fi
-            PTG_LIB=$L run ab_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} || exit $?
+            PTG_LIB=$L run ab_${k}_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} || exit $?
           done
         done ;;
     bench) run bench 1100 python bench.py || exit $? ;;

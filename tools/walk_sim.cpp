@@ -32,7 +32,7 @@ using namespace ptg::hm;
 
 namespace {
 
-struct Query { f3 o, d; float tmin, tmax; uint32_t subframe; bool any; };
+struct Query { f3 o, d; float tmin, tmax; uint32_t subframe; bool any; uint32_t round = 0; uint32_t src = 0; };
 struct Res {
     float t = -1.0f, u = 0, v = 0;
     uint32_t inst = 0xFFFFFFFFu, prim = 0;
@@ -179,6 +179,7 @@ constexpr uint32_t POP = 0xFFFFFFFFu;
 bool g_spec = true;   // SPEC=0: no parked triangles
 std::set<uint64_t>* g_visits = nullptr;   // PACKET=1: the (instance, block) pairs a query steps
 uint64_t g_last_block = ~0ull;              // the (instance, block) pair the last node step stepped
+std::vector<uint64_t>* g_lines = nullptr;  // CACHESIM: the 128-byte lines a step reads
 
 struct Packed {
     std::vector<BlockCopy> E;          // the device block buffer: [BLAS blocks][TLAS blocks]
@@ -249,6 +250,44 @@ struct SimWalker {
             }
             if(cur & kBeLeaf) { park(); return 0; }
         }
+        return block_step();
+    }
+    // The device's node phase (path_tracer.h node_pop + node_block) with up
+    // to K pops: K = 1 is the shipped kernel (a culled entry or a parked
+    // triangle costs the lane its phase).  `loaded`: the phase read a block.
+    int dev_node_phase(int K, bool& loaded)
+    {
+        loaded = false;
+        for(int k = 0; k < K && cur == kBePop; ++k)
+        {
+            if(stack.size() == (axis < 0 ? 0u : bsp))
+            {
+                if(axis < 0) return 1;
+                if(pend != kBePop) return 0;
+                axis = -1; org = q.o; dir = q.d; inv = winv;
+                if(stack.empty()) return 1;
+            }
+            const auto e = stack.back();
+            stack.pop_back();
+            st.pops++;
+            float n;
+            memcpy(&n, &e.second, 4);
+            static const bool nonear = getenv("NONEAR") != nullptr;   // 4-byte entries: blocks popped without their near test
+            if(!(n < tmax) && !(nonear && !(e.first & kBeLeaf))) continue;
+            cur = e.first;
+            cnear = n;
+            if(cur & kBeLeaf)
+            {
+                park();
+                if(at_leaf()) return 0;
+            }
+        }
+        if(cur == kBePop || at_leaf()) return 0;
+        loaded = true;
+        return block_step();
+    }
+    int block_step()
+    {
         st.steps++;
         st.block_steps++;
         st.bytes += 128;
@@ -256,6 +295,7 @@ struct SimWalker {
         g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur;
         // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
         const BlockCopy& bc = pk.E[size_t(cur) * kBlockCopies + octant(dir)];
+        if(g_lines) g_lines->push_back(size_t(cur) * kBlockCopies + octant(dir));   // one 128 B copy
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
@@ -295,6 +335,7 @@ struct SimWalker {
         st.leaf_steps++;
         st.tri++;
         st.bytes += 48;
+        if(g_lines) g_lines->push_back((1ull << 40) + (uint64_t(b.in->m.index_offset / 3 + id) * 48) / 128);   // TriRec
         Res c;
         if(tri(b, v, id, q.tmin, tmax, c))
         {
@@ -324,6 +365,7 @@ struct SimWalker {
             st.leaf_steps++;
             st.enters++;
             st.bytes += 64;
+            if(g_lines) g_lines->push_back((2ull << 40) + id / 2);   // InstTrav, 64 B
             const ptg_tlas_instance& in = v.instances[id];
             b = enter(in, id, q.o, q.d);
             axis = b.axis; bsp = uint32_t(stack.size());
@@ -518,10 +560,19 @@ int main(int argc, char** argv)
 
     // the query mix
     std::vector<Query> qs;
+    const bool tiled = getenv("CACHESIM") != nullptr;   // paths in the device's queue order: 8 pixels x 8 samples per wave
+    const uint32_t x0 = uint32_t(rnd() * (cfg.width / 2)), y0 = uint32_t(rnd() * (cfg.height / 2));
     for(uint32_t p = 0; p < paths; ++p)
     {
-        const uint32_t px = uint32_t(rnd() * cfg.width), py = uint32_t(rnd() * cfg.height);
-        const uint32_t sf = uint32_t(rnd() * v.subframe_count) % v.subframe_count;
+        uint32_t px = uint32_t(rnd() * cfg.width), py = uint32_t(rnd() * cfg.height);
+        uint32_t sf = uint32_t(rnd() * v.subframe_count) % v.subframe_count;
+        if(tiled)
+        {   // wave g = p / 64: pixels 8 (g % 80) .. +7 of row y0 + g / 80; lane: pixel (p % 64) / 8, sample p % 8
+            const uint32_t g = p / 64, lane = p % 64;
+            px = (x0 + 8 * (g % 80) + lane / 8) % cfg.width;
+            py = (y0 + g / 80) % cfg.height;
+            sf = (g * 8 / 8) % v.subframe_count;
+        }
         const ptg_camera& cam = v.subframes[sf].cam;
         float ux = (px + 0.5f) / cfg.width * 2.0f - 1.0f, uy = (py + 0.5f) / cfg.height * 2.0f - 1.0f;
         ux *= cam.aspect_ratio;
@@ -529,22 +580,271 @@ int main(int argc, char** argv)
         f3 d = normalize(v3(ux * cam.inv_focal_length, uy * cam.inv_focal_length, -1.0f));
         d = mul_m3v3(cam.orientation, d);
         f3 o = cam.position;
+        uint32_t src = 0xFFFFu;   // the instance the ray leaves (camera: none)
         for(uint32_t bnc = 0; bnc <= 4; ++bnc)
         {
-            Query q{o, d, bnc ? 1e-4f : 0.0f, 1e9f, sf, false};
+            Query q{o, d, bnc ? 1e-4f : 0.0f, 1e9f, sf, false, bnc, src};
             qs.push_back(q);
             Stats tmp;
             Res r = link_walk(v, q, tmp);
             if(r.inst == 0xFFFFFFFFu) break;
             o = o + d * r.t;
             f3 L = normalize(v.subframes[sf].light.direction);
-            qs.push_back(Query{o, L, 1e-4f, 1e9f, sf, true});
+            src = r.inst;
+            qs.push_back(Query{o, L, 1e-4f, 1e9f, sf, true, bnc, src});
             f3 nd;
             do { nd = v3(rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1); } while(dot(nd, nd) > 1 || dot(nd, nd) < 1e-4f);
             nd = normalize(nd);
             if(dot(nd, d) > 0) nd = -nd;
             d = nd;
         }
+    }
+    if(const char* cs = getenv("CACHESIM"))
+    {   // Cache behaviour of the walk kernel's access stream on one slice of
+        // an XCD: W lockstep waves (12 per CU) stepping round-robin, wave w
+        // taking the queue's 64-entry groups w, w + W, ... of each round (the
+        // kernel's static split), 2 node phases + 1 leaf phase per
+        // iteration, refill at 24 idle lanes.  Each lane's 128 B lines go
+        // through its CU's L1 (32 KB, 64-way LRU sets) and the slice's share of
+        // L2 (4 MB per 32 CUs, 16-way).  CACHESIM="order": 0 queue order,
+        // 1 each round's queue sorted by ray octant (stable).
+        const int order = atoi(cs);
+        const int W = 96, per_cu = 12;
+        struct Cache {
+            uint32_t sets, ways;
+            std::vector<uint64_t> tag, age;
+            uint64_t clock = 0, hits = 0, miss = 0;
+            Cache(uint32_t lines, uint32_t w) : sets(lines / w), ways(w), tag(size_t(lines), ~0ull), age(size_t(lines), 0) {}
+            bool access(uint64_t line)
+            {
+                const size_t s0 = size_t(line % sets) * ways;
+                ++clock;
+                size_t lru = s0;
+                for(size_t k = s0; k < s0 + ways; ++k)
+                {
+                    if(tag[k] == line) { age[k] = clock; ++hits; return true; }
+                    if(age[k] < age[lru]) lru = k;
+                }
+                tag[lru] = line; age[lru] = clock; ++miss;
+                return false;
+            }
+        };
+        for(int any = 0; any < 2; ++any)
+        {
+            std::vector<Cache> l1(W / per_cu, Cache(256, 64));
+            Cache l2(uint32_t((4u << 20) / 128 * (W / per_cu) / 32), 16);
+            double node_ph = 0, leaf_ph = 0, nq = 0;
+            for(uint32_t rd = 0; rd <= 4; ++rd)
+            {
+                std::vector<const Query*> qq;
+                for(const Query& q: qs)
+                    if(q.any == bool(any) && q.round == rd) qq.push_back(&q);
+                if(order == 1)
+                    std::stable_sort(qq.begin(), qq.end(), [](const Query* a, const Query* b) { return octant(a->d) < octant(b->d); });
+                else if(order == 4 || order == 5)
+                {   // octant-sorted within each run of 256 (a shade block's append) or 2048 queue entries
+                    const size_t run = order == 4 ? 256 : 2048;
+                    for(size_t i = 0; i < qq.size(); i += run)
+                        std::stable_sort(qq.begin() + i, qq.begin() + std::min(qq.size(), i + run),
+                                         [](const Query* a, const Query* b) { return octant(a->d) < octant(b->d); });
+                }
+                else if(order == 7 || order == 8)
+                {   // the device's key: 12-bit Morton hash of the origin's cell (CELL metres), ties by queue order;
+                    // 8: the octant and a 9-bit hash
+                    static const float cell = getenv("CELL") ? float(atof(getenv("CELL"))) : 2.0f;
+                    auto key = [&](const Query* q) {
+                        auto sp = [](int32_t c) {
+                            uint32_t x = uint32_t(c) & 15u;
+                            x = (x | (x << 4)) & 0x0C3u; x = (x | (x << 2)) & 0x249u;
+                            return x;
+                        };
+                        const int32_t cx = int32_t(std::floor(q->o.x / cell)), cy = int32_t(std::floor(q->o.y / cell)),
+                                      cz = int32_t(std::floor(q->o.z / cell));
+                        const uint32_t m = sp(cx) | (sp(cy) << 1) | (sp(cz) << 2);
+                        return order == 7 ? m : (octant(q->d) << 9) | (m & 511u);
+                    };
+                    std::stable_sort(qq.begin(), qq.end(), [&](const Query* a, const Query* b) { return key(a) < key(b); });
+                }
+                else if(order == 6)
+                    std::stable_sort(qq.begin(), qq.end(), [](const Query* a, const Query* b) {
+                        return (uint64_t(octant(a->d)) << 32 | a->src) < (uint64_t(octant(b->d)) << 32 | b->src); });
+                else if(order >= 2 && !qq.empty())
+                {   // Morton order of the ray origins (10 bits per axis over the round's origin bounds), octant first (2) or not (3)
+                    f3 lo = qq[0]->o, hi = qq[0]->o;
+                    for(const Query* q: qq)
+                    {
+                        lo = v3(std::min(lo.x, q->o.x), std::min(lo.y, q->o.y), std::min(lo.z, q->o.z));
+                        hi = v3(std::max(hi.x, q->o.x), std::max(hi.y, q->o.y), std::max(hi.z, q->o.z));
+                    }
+                    auto spread = [](uint64_t x) {
+                        x &= 0x3FF;
+                        x = (x | (x << 16)) & 0x030000FF; x = (x | (x << 8)) & 0x0300F00F;
+                        x = (x | (x << 4)) & 0x030C30C3; x = (x | (x << 2)) & 0x09249249;
+                        return x;
+                    };
+                    auto key = [&](const Query* q) {
+                        auto qz = [](float a, float l, float h) { return uint64_t(std::min(1023.0f, (a - l) / std::max(h - l, 1e-20f) * 1024.0f)); };
+                        const uint64_t m = spread(qz(q->o.x, lo.x, hi.x)) | (spread(qz(q->o.y, lo.y, hi.y)) << 1) | (spread(qz(q->o.z, lo.z, hi.z)) << 2);
+                        return order == 2 ? (uint64_t(octant(q->d)) << 30) | m : m;
+                    };
+                    std::stable_sort(qq.begin(), qq.end(), [&](const Query* a, const Query* b) { return key(a) < key(b); });
+                }
+                nq += double(qq.size());
+                const size_t groups = (qq.size() + 63) / 64;
+                struct WaveSt { std::vector<std::unique_ptr<SimWalker>> lane; std::vector<Stats> st; size_t g, used; };
+                std::vector<WaveSt> ws(W);
+                for(int w = 0; w < W; ++w) { ws[w].lane.resize(64); ws[w].st.resize(64); ws[w].g = size_t(w); ws[w].used = 0; }
+                auto next_query = [&](WaveSt& x) -> const Query* {
+                    while(x.g < groups)
+                    {
+                        const size_t i = x.g * 64 + x.used;
+                        if(x.used < 64 && i < qq.size()) { ++x.used; return qq[i]; }
+                        x.g += W; x.used = 0;
+                    }
+                    return nullptr;
+                };
+                std::vector<uint64_t> lines;
+                g_lines = &lines;
+                for(bool live = true; live;)
+                {
+                    live = false;
+                    for(int w = 0; w < W; ++w)
+                    {
+                        WaveSt& x = ws[w];
+                        Cache& c1 = l1[w / per_cu];
+                        int idle = 0;
+                        for(auto& l: x.lane) idle += l ? 0 : 1;
+                        if(idle >= 24 || idle == 64)
+                            for(int k = 0; k < 64; ++k)
+                                if(!x.lane[k])
+                                    if(const Query* q = next_query(x)) x.lane[k].reset(new SimWalker(v, pk, *q, x.st[k], S, g_spec));
+                        bool any_live = false;
+                        for(auto& l: x.lane) any_live = any_live || bool(l);
+                        if(!any_live) continue;
+                        live = true;
+                        auto feed = [&](double& ph) {
+                            if(lines.empty()) return;
+                            ph += 1;
+                            for(uint64_t ln: lines)
+                                if(!c1.access(ln)) l2.access(ln);
+                            lines.clear();
+                        };
+                        for(int u = 0; u < 2; ++u)
+                        {
+                            for(auto& l: x.lane)
+                            {
+                                if(!l || l->at_leaf()) continue;
+                                bool ld;
+                                if(l->dev_node_phase(1, ld)) l.reset();
+                            }
+                            feed(node_ph);
+                        }
+                        for(auto& l: x.lane)
+                            if(l && l->wants_leaf() && l->leaf_step()) l.reset();
+                        feed(leaf_ph);
+                    }
+                }
+                g_lines = nullptr;
+            }
+            uint64_t h1 = 0, m1 = 0;
+            for(auto& c: l1) { h1 += c.hits; m1 += c.miss; }
+            printf("cachesim %s order=%d: %.0f queries, L1 hit %.1f%%, L2 hit %.1f%% of L1 misses, L2 misses %.2f per query, L1 misses %.2f per query\n",
+                   any ? "any" : "closest", order, nq, 100.0 * h1 / double(h1 + m1), 100.0 * l2.hits / double(l2.hits + l2.miss),
+                   l2.miss / nq, m1 / nq);
+        }
+        return 0;
+    }
+    if(const char* ls = getenv("LOCKSTEP"))
+    {   // the wavefront walk kernel's lockstep schedule over the query mix,
+        // per walk kind, in waves of 64 lanes with the kernel's refill rule:
+        // vector-memory instructions (7 per node phase that reads a block, 4
+        // per leaf phase that reads a record, 3 per refill) and the lanes each
+        // serves.  LOCKSTEP="U K T": U node phases per leaf phase, K pops per
+        // node phase, leaf phase only when >= T lanes want one (or no lane
+        // can take a node step).
+        int U = 2, K = 1, T = 1, R = 24;
+        sscanf(ls, "%d %d %d %d", &U, &K, &T, &R);
+        for(int any = 0; any < 2; ++any)
+        {
+            std::vector<const Query*> mine;
+            for(const Query& q: qs)
+                if(q.any == bool(any)) mine.push_back(&q);
+            double ni = 0, nl = 0, li = 0, ll = 0, ri = 0, rl = 0, phases = 0, iters = 0, waves = 0, act = 0, leaf_ph = 0, leaf_ph_enter = 0, rph = 0;
+            const size_t per_wave = 4096;   // queries one wave works through (its range)
+            uint64_t lmism = 0;
+            double why[5] = {};   // node-phase lanes not reading a block: instance leaf, triangle leaf, parked & waiting, popped nothing steppable, empty
+            auto check = [&](const SimWalker& w) {   // every finished walk against the reference's link walk
+                Stats tmp;
+                if(!(link_walk(v, w.q, tmp) == w.best)) ++lmism;
+            };
+            for(size_t w0 = 0; w0 < mine.size(); w0 += per_wave)
+            {
+                const size_t end = std::min(mine.size(), w0 + per_wave);
+                size_t next = w0;
+                std::vector<Stats> lst(64);
+                std::vector<std::unique_ptr<SimWalker>> lane(64);
+                waves++;
+                for(;;)
+                {
+                    int idle = 0;
+                    for(auto& l: lane) idle += l ? 0 : 1;
+                    if(next < end && (idle >= R || idle == 64))
+                    {
+                        int took = 0;
+                        for(int k = 0; k < 64 && next < end; ++k)
+                            if(!lane[k]) { lane[k].reset(new SimWalker(v, pk, *mine[next++], lst[k], S, g_spec)); ++took; }
+                        ri += 3; rl += 3 * took; rph++;
+                    }
+                    int live = 0;
+                    for(auto& l: lane) live += l ? 1 : 0;
+                    if(!live) break;
+                    iters++;
+                    act += live;
+                    for(int u = 0; u < U; ++u)
+                    {
+                        int loads = 0;
+                        for(auto& l: lane)
+                        {
+                            if(l && l->at_leaf()) { why[l->axis < 0 ? 0 : 1]++; continue; }
+                            if(!l) { why[4]++; continue; }
+                            bool ld;
+                            if(l->dev_node_phase(K, ld)) { check(*l); l.reset(); }
+                            loads += ld ? 1 : 0;
+                            if(l && !ld) why[l->pend != kBePop && l->cur == kBePop ? 2 : 3]++;
+                        }
+                        if(loads) { ni += 7; nl += 7 * loads; phases++; }
+                    }
+                    int want = 0, can_node = 0;
+                    for(auto& l: lane)
+                        if(l) { want += l->wants_leaf() ? 1 : 0; can_node += l->at_leaf() ? 0 : 1; }
+                    if(want && (want >= T || can_node == 0 || want == live))
+                    {
+                        int loads = 0, enters = 0;
+                        for(auto& l: lane)
+                        {
+                            if(!l || !l->wants_leaf()) continue;
+                            const double before = l->st.tri + l->st.enters, e0 = l->st.enters;
+                            const int r = l->leaf_step();
+                            loads += (l->st.tri + l->st.enters > before) ? 1 : 0;
+                            enters += (l->st.enters > e0) ? 1 : 0;
+                            if(r) { check(*l); l.reset(); }
+                        }
+                        if(loads) { li += 4; ll += 4 * loads; phases++; leaf_ph++; leaf_ph_enter += enters ? 1 : 0; }
+                    }
+                }
+            }
+            const double nq = double(mine.size());
+            printf("lockstep %s U=%d K=%d T=%d: per query %.2f VMEM (node %.2f, leaf %.2f, refill %.2f), %.1f phases with loads per wave-query64, lanes/instr node %.1f leaf %.1f, active %.1f\n",
+                   any ? "any" : "closest", U, K, T, (ni + li + ri) * 64 / nq, ni * 64 / nq, li * 64 / nq, ri * 64 / nq,
+                   phases * 64 / nq, nl / std::max(ni, 1.0), ll / std::max(li, 1.0), act / std::max(iters, 1.0));
+            const double tot_ph = ni / 7;
+            printf("  per node phase, lanes not reading: at instance %.1f, at triangle %.1f, parked+stalled %.1f, popped none %.1f, empty %.1f\n",
+                   why[0] / tot_ph, why[1] / tot_ph, why[2] / tot_ph, why[3] / tot_ph, why[4] / tot_ph);
+            printf("  refill phases %.2f per wave-query64 (R=%d)\n", rph * 64 / nq, R);
+            printf("  leaf phases with a BLAS entry: %.1f%%; %llu mismatches vs the link walk\n",
+                   100.0 * leaf_ph_enter / std::max(leaf_ph, 1.0), (unsigned long long)lmism);
+        }
+        return 0;
     }
     Stats sl[2], sb[2];
     uint64_t mism = 0;
