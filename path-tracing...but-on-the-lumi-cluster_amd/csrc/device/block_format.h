@@ -62,7 +62,10 @@
 
 namespace ptg {
 
-constexpr uint32_t kBlockWidth = 4;
+#ifndef PTG_BLOCK_WIDTH
+#define PTG_BLOCK_WIDTH 4   // other widths only in the CPU model (tools/walk_sim, WIDTH=8)
+#endif
+constexpr uint32_t kBlockWidth = PTG_BLOCK_WIDTH;
 constexpr uint32_t kBlockCopies = 8;   // a block: one copy per octant
 
 struct alignas(16) BlockCopy {
@@ -71,9 +74,10 @@ struct alignas(16) BlockCopy {
         uint32_t a;
     } n[kBlockWidth];                  // rows 0-3
     float f[3 * kBlockWidth];          // rows 4-6: entry j's far planes at f[3j .. 3j+2]
-    uint32_t pad[4];                   // row 7 (keeps copies on 128-byte lines)
+    uint32_t pad[(128 - (28 * kBlockWidth) % 128) % 128 / 4];   // row 7 (keeps copies on 128-byte lines)
 };
-static_assert(sizeof(BlockCopy) == 128, "BlockCopy is one 128-byte line");
+static_assert(sizeof(BlockCopy) % 128 == 0 && (kBlockWidth != 4 || sizeof(BlockCopy) == 128),
+              "BlockCopy is one 128-byte line");
 
 constexpr uint32_t kBeLeaf = 0x80000000u;
 constexpr uint32_t kBeNone = 0x40000000u;

@@ -211,7 +211,7 @@ struct LdsCold {
 // the per-ray entry points; the host checks every frame's stack bound
 // against kCap before those kernels run.
 struct PrivStack {
-    static constexpr uint32_t kCap = 96;     // entries; put() may write one past the bound
+    static constexpr uint32_t kCap = kBlockWidth > 4 ? 128 : 96;   // entries; put() may write one past the bound
     uint2 v[kCap];
     uint32_t sp;
     PTG_D void reset() { sp = 0; }
@@ -477,60 +477,93 @@ struct BlockWalker {
         return -1;
     }
 
-    // this octant's copy of block cur: its four entries in the order the ray
-    // meets them, each box as (near planes, far planes) for the octant's
-    // signs; seven 16-byte rows
+    // this octant's copy of block cur: its kBlockWidth entries in the order
+    // the ray meets them, each box as (near planes, far planes) for the
+    // octant's signs; kBlockRows 16-byte rows (seven at width 4)
+    static constexpr uint32_t kBlockRows = (28u * kBlockWidth + 15u) / 16u;
     PTG_D const v4f* block_rows(const DevScene& sc) const
     {
         return reinterpret_cast<const v4f*>(sc.blocks + size_t(cur) * kBlockCopies + oct);
     }
-
-    // Node phase, second half: the block step on its seven rows.
-    template<bool COUNT>
-    PTG_D int node_block(const DevScene& sc, Counters& cnt, v4f q0, v4f q1, v4f q2, v4f q3, v4f q4, v4f q5, v4f q6)
+    // float k of the packed far planes (rows kBlockWidth..): entry j's at 3j..3j+2
+    static PTG_D float far_plane(const v4f* q, uint32_t k)
     {
-        // rows 0-3: entry j's near planes and word; rows 4-6: the far planes, packed
-        const float4 l0 = make_float4(q0.x, q0.y, q0.z, q0.w), h0 = make_float4(q4.x, q4.y, q4.z, 0.0f);
-        const float4 l1 = make_float4(q1.x, q1.y, q1.z, q1.w), h1 = make_float4(q4.w, q5.x, q5.y, 0.0f);
-        const float4 l2 = make_float4(q2.x, q2.y, q2.z, q2.w), h2 = make_float4(q5.z, q5.w, q6.x, 0.0f);
-        const float4 l3 = make_float4(q3.x, q3.y, q3.z, q3.w), h3 = make_float4(q6.y, q6.z, q6.w, 0.0f);
+        const v4f r = q[kBlockWidth + k / 4u];
+        const uint32_t c = k % 4u;
+        return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w;
+    }
+
+    // Node phase, second half: the block step on its rows.
+    template<bool COUNT>
+    PTG_D int node_block(const DevScene& sc, Counters& cnt, const v4f (&q)[kBlockRows])
+    {
+        // rows 0..W-1: entry j's near planes and word; then the far planes, packed
+        constexpr uint32_t W = kBlockWidth;
+        float4 l[W], h[W];
+        uint32_t a[W];
+        float nr[W];
+        bool pass[W];
+#pragma unroll
+        for(uint32_t j = 0; j < W; ++j)
+        {
+            l[j] = make_float4(q[j].x, q[j].y, q[j].z, q[j].w);
+            h[j] = make_float4(far_plane(q, 3 * j), far_plane(q, 3 * j + 1), far_plane(q, 3 * j + 2), 0.0f);
+            a[j] = __float_as_uint(l[j].w);
+        }
         if(COUNT) cnt.step_loads |= 1u;
-        const uint32_t a0 = __float_as_uint(l0.w), a1 = __float_as_uint(l1.w), a2 = __float_as_uint(l2.w),
-                       a3 = __float_as_uint(l3.w);
-        float n0, n1, n2, n3;
-        bool p0, p1, p2, p3;
         if(__all(fin))
         {   // every lane's reciprocal finite (the rule): no per-axis min/max
-            p0 = box_near_far(l0, h0, n0); p1 = box_near_far(l1, h1, n1);
-            p2 = box_near_far(l2, h2, n2); p3 = box_near_far(l3, h3, n3);
+#pragma unroll
+            for(uint32_t j = 0; j < W; ++j) pass[j] = box_near_far(l[j], h[j], nr[j]);
         }
         else
         {   // a lane with a zero or denormal direction component: the
             // reference's min/max form (an unordered pair gives the same)
-            p0 = box(l0, h0, n0); p1 = box(l1, h1, n1); p2 = box(l2, h2, n2); p3 = box(l3, h3, n3);
+#pragma unroll
+            for(uint32_t j = 0; j < W; ++j) pass[j] = box(l[j], h[j], nr[j]);
         }
         if(COUNT)
         {
-            const uint32_t tested = !(a0 & kBeNone) + !(a1 & kBeNone) + !(a2 & kBeNone) + !(a3 & kBeNone);
+            uint32_t tested = 0;
+#pragma unroll
+            for(uint32_t j = 0; j < W; ++j) tested += !(a[j] & kBeNone);
             cnt.visits += tested;
             if(axis < 0) cnt.tlas_visits += tested;
         }
         // bit j: the entry the ray meets j-th passed.  The first is walked
         // next; the others are pushed last-first, so they pop in order.
-        const uint32_t hits = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
-        const uint32_t first = uint32_t(__builtin_ctz(hits | 16u)) & 3u;
-        cur = hits ? sel4(first, a0, a1, a2, a3) : kBePop;
-        cnear = __uint_as_float(sel4(first, __float_as_uint(n0), __float_as_uint(n1), __float_as_uint(n2),
-                                     __float_as_uint(n3)));
+        uint32_t hits = 0;
+#pragma unroll
+        for(uint32_t j = 0; j < W; ++j) hits |= pass[j] ? (1u << j) : 0u;
+        const uint32_t first = uint32_t(__builtin_ctz(hits | (1u << W))) & (W - 1u);
+        uint32_t fa, fn;   // entry `first`, by value (v_cndmask): neither a branch nor an indexed copy
+        if constexpr(W == 4)
+        {
+            fa = sel4(first, a[0], a[1], a[2], a[3]);
+            fn = sel4(first, __float_as_uint(nr[0]), __float_as_uint(nr[1]), __float_as_uint(nr[2]),
+                      __float_as_uint(nr[3]));
+        }
+        else
+        {
+            fa = a[0];
+            fn = __float_as_uint(nr[0]);
+#pragma unroll
+            for(uint32_t j = 1; j < W; ++j)
+            {
+                fa = first == j ? a[j] : fa;
+                fn = first == j ? __float_as_uint(nr[j]) : fn;
+            }
+        }
+        cur = hits ? fa : kBePop;
+        cnear = __uint_as_float(fn);
         const uint32_t rest = hits & (hits - 1u);
         if(rest)
         {   // written at the top either way, kept only if pushed
             // (the host's stack bound, which sizes the spill areas, must hold)
             PTG_CHECK(sc, st.size() + uint32_t(__builtin_popcount(rest)) <= sc.spill_stride, kDebugStack);
-            st.reserve(kBlockWidth - 1);
-            st.put(make_uint2(a3, __float_as_uint(n3)), (rest >> 3) & 1u);
-            st.put(make_uint2(a2, __float_as_uint(n2)), (rest >> 2) & 1u);
-            st.put(make_uint2(a1, __float_as_uint(n1)), (rest >> 1) & 1u);
+            st.reserve(W - 1);
+#pragma unroll
+            for(uint32_t j = W - 1; j >= 1; --j) st.put(make_uint2(a[j], __float_as_uint(nr[j])), (rest >> j) & 1u);
         }
         park();
         return 0;
@@ -545,7 +578,10 @@ struct BlockWalker {
         if(const int r = node_pop(); r >= 0) return r;
         PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
         const v4f* p = block_rows(sc);
-        return node_block<COUNT>(sc, cnt, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        v4f q[kBlockRows];
+#pragma unroll
+        for(uint32_t k = 0; k < kBlockRows; ++k) q[k] = p[k];
+        return node_block<COUNT>(sc, cnt, q);
     }
 
     // Leaf phase, first half: the parked triangle, else the BLAS entry or

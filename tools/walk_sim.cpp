@@ -295,7 +295,9 @@ struct SimWalker {
         g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur;
         // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
         const BlockCopy& bc = pk.E[size_t(cur) * kBlockCopies + octant(dir)];
-        if(g_lines) g_lines->push_back(size_t(cur) * kBlockCopies + octant(dir));   // one 128 B copy
+        if(g_lines)   // the copy's 128 B lines
+            for(size_t k = 0; k < sizeof(BlockCopy) / 128; ++k)
+                g_lines->push_back((size_t(cur) * kBlockCopies + octant(dir)) * (sizeof(BlockCopy) / 128) + k);
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
@@ -762,6 +764,7 @@ int main(int argc, char** argv)
         // serves.  LOCKSTEP="U K T": U node phases per leaf phase, K pops per
         // node phase, leaf phase only when >= T lanes want one (or no lane
         // can take a node step).
+        const double kRows = (28.0 * kBlockWidth + 15) / 16;   // 16-byte rows a block step reads (7 at width 4)
         int U = 2, K = 1, T = 1, R = 24;
         sscanf(ls, "%d %d %d %d", &U, &K, &T, &R);
         for(int any = 0; any < 2; ++any)
@@ -812,7 +815,7 @@ int main(int argc, char** argv)
                             loads += ld ? 1 : 0;
                             if(l && !ld) why[l->pend != kBePop && l->cur == kBePop ? 2 : 3]++;
                         }
-                        if(loads) { ni += 7; nl += 7 * loads; phases++; }
+                        if(loads) { ni += kRows; nl += kRows * loads; phases++; }
                     }
                     int want = 0, can_node = 0;
                     for(auto& l: lane)
@@ -837,7 +840,7 @@ int main(int argc, char** argv)
             printf("lockstep %s U=%d K=%d T=%d: per query %.2f VMEM (node %.2f, leaf %.2f, refill %.2f), %.1f phases with loads per wave-query64, lanes/instr node %.1f leaf %.1f, active %.1f\n",
                    any ? "any" : "closest", U, K, T, (ni + li + ri) * 64 / nq, ni * 64 / nq, li * 64 / nq, ri * 64 / nq,
                    phases * 64 / nq, nl / std::max(ni, 1.0), ll / std::max(li, 1.0), act / std::max(iters, 1.0));
-            const double tot_ph = ni / 7;
+            const double tot_ph = ni / kRows;
             printf("  per node phase, lanes not reading: at instance %.1f, at triangle %.1f, parked+stalled %.1f, popped none %.1f, empty %.1f\n",
                    why[0] / tot_ph, why[1] / tot_ph, why[2] / tot_ph, why[3] / tot_ph, why[4] / tot_ph);
             printf("  refill phases %.2f per wave-query64 (R=%d)\n", rph * 64 / nq, R);
