@@ -41,3 +41,27 @@ def test_block_walk_matches_link_walk(walk_sim, assets_dir, frame):
     # deduplication): ~50 MB of per-subframe blocks become 1-2 MB
     t = re.search(r"TLAS (\d+) copies \(([0-9.]+) MB\)", r.stdout)
     assert t and float(t.group(2)) < 5.0, r.stdout
+
+
+def test_lockstep_schedule_model_exact(walk_sim, assets_dir):
+    """The model of the kernel's lockstep schedule (tools/walk_sim LOCKSTEP,
+    DESIGN.md section 4.2) walks every query to the reference's result and
+    reports the lanes each load serves."""
+    env = dict(os.environ, LOCKSTEP="2 1 1 24")
+    r = subprocess.run([walk_sim, assets_dir, "450", "1500", "16"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert len(re.findall(r"; 0 mismatches vs the link walk", r.stdout)) == 2, r.stdout
+    lanes = [float(x) for x in re.findall(r"lanes/instr node ([0-9.]+)", r.stdout)]
+    assert len(lanes) == 2 and all(20 < x < 64 for x in lanes), r.stdout
+
+
+def test_eight_wide_blocks_exact(native_lib, assets_dir):
+    """8-wide blocks (measured slower on the GPU) meet
+    every leaf in the reference's order too: the packer and the walk are
+    generic in the block width."""
+    subprocess.run(["make", "-s", "walk_sim8"], cwd=os.path.join(ROOT, "tools"), check=True)
+    r = subprocess.run([os.path.join(ROOT, "tools", "_bin", "walk_sim8"), assets_dir, "450", "1500", "16"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
+    assert m and int(m.group(2)) == 0, r.stdout
