@@ -482,8 +482,11 @@ struct BlockWalker {
     // octant's signs; kBlockRows 16-byte rows (seven at width 4)
     static constexpr uint32_t kBlockRows = (28u * kBlockWidth + 15u) / 16u;
     PTG_D const v4f* block_rows(const DevScene& sc) const
-    {
-        return reinterpret_cast<const v4f*>(sc.blocks + size_t(cur) * kBlockCopies + oct);
+    {   // a 32-bit byte offset from the buffer's base (the upload keeps the
+        // block buffer below 4 GB), so the loads take the scalar-base +
+        // vector-offset form instead of 64-bit address arithmetic per lane
+        const uint32_t off = (cur * kBlockCopies + oct) * uint32_t(sizeof(BlockCopy));
+        return reinterpret_cast<const v4f*>(reinterpret_cast<const uint8_t*>(sc.blocks) + off);
     }
     // float k of the packed far planes (rows kBlockWidth..): entry j's at 3j..3j+2
     static PTG_D float far_plane(const v4f* q, uint32_t k)
@@ -602,8 +605,12 @@ struct BlockWalker {
         else cur = kBePop;
         ls.inst_leaf = !ls.parked && axis < 0;
         ls.tri = !ls.inst_leaf && n < tmax;
-        ls.p = ls.inst_leaf ? reinterpret_cast<const v4f*>(sc.inst_trav + ls.id)
-                            : reinterpret_cast<const v4f*>(sc.tris + tri_base + ls.id);
+        // 32-bit byte offsets (the triangle records stay below 4 GB: checked
+        // at upload) instead of 64-bit multiplies per lane
+        const uint8_t* base = ls.inst_leaf ? reinterpret_cast<const uint8_t*>(sc.inst_trav)
+                                           : reinterpret_cast<const uint8_t*>(sc.tris);
+        const uint32_t off = ls.inst_leaf ? ls.id * uint32_t(sizeof(InstTrav)) : (tri_base + ls.id) * uint32_t(sizeof(TriRec));
+        ls.p = reinterpret_cast<const v4f*>(base + off);
         return ls;
     }
 
@@ -640,12 +647,12 @@ struct BlockWalker {
     {
         const LeafSel ls = leaf_select(sc);
         if(ls.inst_leaf) PTG_CHECK(sc, ls.id < sc.inst_count, kDebugInst);
-        if(ls.tri) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);
-        v4f r0 = {0, 0, 0, 0}, r1 = r0, r2 = r0, r3 = r0;
-        if(ls.inst_leaf || ls.tri)
-        {
-            r0 = ls.p[0]; r1 = ls.p[1]; r2 = ls.p[2]; r3 = ls.p[3];
-        }
+        if(!ls.inst_leaf) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);   // read even when culled
+        // every leaf lane reads its record, also a triangle whose deferred
+        // near test failed (its rows then go unused): the record's address is
+        // valid either way, the wave issues the same four loads, and the rows
+        // need no zeroing or branch around the loads
+        const v4f r0 = ls.p[0], r1 = ls.p[1], r2 = ls.p[2], r3 = ls.p[3];
         return leaf_finish<ANY, COUNT>(sc, cnt, ls, r0, r1, r2, r3);
     }
 

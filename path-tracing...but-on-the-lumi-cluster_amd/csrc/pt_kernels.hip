@@ -1437,6 +1437,9 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     PTG_HIP(ctx->normal.reserve(vertex_count * 16));
     PTG_HIP(ctx->albedo.reserve(vertex_count * 16));
     PTG_HIP(ctx->material.reserve(vertex_count * 16));
+    // the walks address triangle records by 32-bit byte offsets (BlockWalker::leaf_select)
+    if(index_count / 3 * sizeof(TriRec) + 128 > 0xFFFFFFFFull)
+        return fail(PTG_E_RANGE, "triangle records above 4 GB (" + std::to_string(index_count / 3) + " triangles)");
     // slack: the walk's leaf phase reads a triangle as four 16-byte rows (the
     // 48-byte record and the next 16 bytes)
     PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 128));
@@ -1515,6 +1518,8 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     const std::vector<BlockCopy>& old_blas = ctx->cache.blas;
     const size_t blas_total = old_blas.size() + fp.new_blas.size();
     const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockCopy);
+    if(need > 0xFFFFFFFFull)   // the walks address blocks by 32-bit byte offsets (BlockWalker::block_rows)
+        return fail(PTG_E_RANGE, "block records above 4 GB (" + std::to_string(need) + " B)");
     if(need > ctx->blocks.bytes)
     {
         PTG_HIP(grow(ctx->blocks, need + need / 8));
