@@ -63,8 +63,12 @@ PTG_D float rcp_nr(float x, bool& ok)
 PTG_D float rcp_rn(float x)
 {
     bool ok = true;
-    const float r = rcp_nr(x, ok);
-    return ok ? r : 1.0f / x;
+    float r = rcp_nr(x, ok);
+    // the IEEE division only in a wave with a lane outside the fast path's
+    // range (zeros, denormals, huge values: rare); written as a plain select
+    // the compiler computed the division on every lane
+    if(!__all(ok)) r = ok ? r : 1.0f / x;
+    return r;
 }
 
 // x / c for a divisor c known at compile time, with rc = RN(1/c): the
