@@ -449,32 +449,33 @@ struct BlockWalker {
     // (0: nothing to step this phase, 1: the walk has ended).
     PTG_D int node_pop()
     {
-        if(cur == kBePop)
-        {   // one pop per node phase, straight-line: a culled entry or a
-            // finished BLAS simply costs the lane its next phase
-            if(st.size() == (axis < 0 ? 0u : bsp))
-            {
-                if(axis < 0) return 1;
-                if(pend != kBePop) return 0;   // its parked triangle needs this BLAS: wait for the leaf phase
-                // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
-                axis = -1;
-                org = cold.world_o();
-                inv = winv;
-                fin = finite3(winv);
-                oct = octant(cold.world_d());
-                if(st.size() == 0) return 1;
-            }
-            const uint2 e = st.pop();
-            if(!(__uint_as_float(e.y) < tmax)) return 0;   // the entry's test at its own time failed
-            cur = e.x;
-            cnear = __uint_as_float(e.y);
-            if(cur & kBeLeaf)
-            {
-                park();
-                return 0;
-            }
+        if(cur != kBePop) return -1;
+        // one pop per node phase: a culled entry or a parked triangle simply
+        // costs the lane its phase.  Straight-line selects after the pop (no
+        // nested early returns: the compiler turned each into exec-mask
+        // bookkeeping on every lane)
+        if(st.size() == (axis < 0 ? 0u : bsp))
+        {   // this level's entries are exhausted (rare)
+            if(axis < 0) return 1;
+            if(pend != kBePop) return 0;   // its parked triangle needs this BLAS: wait for the leaf phase
+            // BLAS exhausted: back to the TLAS (ray_query.hh:273-274)
+            axis = -1;
+            org = cold.world_o();
+            inv = winv;
+            fin = finite3(winv);
+            oct = octant(cold.world_d());
+            if(st.size() == 0) return 1;
         }
-        return -1;
+        const uint2 e = st.pop();
+        const float n = __uint_as_float(e.y);
+        const bool live = n < tmax;                        // the entry's test at its own time
+        const bool leaf = (e.x & kBeLeaf) != 0;
+        const bool parked = live && leaf && axis >= 0 && pend == kBePop;   // park() of the popped triangle
+        pend = parked ? e.x : pend;
+        pnear = parked ? n : pnear;
+        cur = live && !parked ? e.x : kBePop;
+        cnear = n;
+        return live && !leaf ? -1 : 0;                     // a block to step now, else nothing this phase
     }
 
     // this octant's copy of block cur: its kBlockWidth entries in the order
