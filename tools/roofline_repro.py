@@ -16,7 +16,7 @@ time taken two ways:
 and checks that its numbers equal the bench line's (1e-3 relative) and that
 the two launch times agree (15%, the bench's own acceptance rule).
 
-Usage: roofline_repro.py [bench_line.json]   (default: the newest profiles/*/bench_line.json)
+Usage: roofline_repro.py [bench_line.json]   (default: the newest profiles/*/bench_line.json with a profile-backed roofline)
 """
 import csv
 import glob
@@ -50,8 +50,11 @@ def levels_of(ent, ceil):
 
 
 def main():
-    path = sys.argv[1] if len(sys.argv) > 1 else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line.json")),
-                                                         key=natural)[-1]
+    if len(sys.argv) > 1:
+        path = sys.argv[1]
+    else:   # the newest bench line whose roofline cites a committed PMC profile (config runs without one are skipped)
+        path = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line.json")), key=natural)
+                if "traffic_source" in (json.load(open(p)).get("roofline") or {})][-1]
     line = json.load(open(path))
     rf = line["roofline"]
     prof_path = os.path.join(ROOT, rf["traffic_source"].split(" ")[0])
