@@ -235,6 +235,64 @@ def cpu_baseline(assets, frame, heavy_frame):
     return out
 
 
+def libm_identity():
+    """The host C library the reference's results depend on: glibc's version,
+    whether its ifuncs take the FMA builds of exp / pow / sin / cos (glibc 2.35
+    picks __exp_fma etc. when the CPU has FMA and AVX2; the device restates
+    those, csrc/device/glibc_math.h), and libm's file hash."""
+    import ctypes.util
+    import hashlib
+    out = {}
+    try:
+        out["glibc"] = os.confstr("CS_GNU_LIBC_VERSION")
+    except (ValueError, OSError):
+        out["glibc"] = None
+    flags = set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        pass
+    out["cpu_fma"] = "fma" in flags
+    out["cpu_avx2"] = "avx2" in flags
+    out["variant"] = "fma (__exp_fma, __pow_fma, __sin_fma, __cos_fma)" if out["cpu_fma"] and out["cpu_avx2"] \
+        else "non-fma (the GPU's restatement is of the FMA builds: the reference would differ)"
+    name = ctypes.util.find_library("m")
+    for d in ("/lib/x86_64-linux-gnu", "/usr/lib/x86_64-linux-gnu"):
+        p = os.path.join(d, "libm.so.6")
+        if os.path.exists(p):
+            with open(p, "rb") as fh:
+                out["libm"] = {"path": p, "sha256_16": hashlib.sha256(fh.read()).hexdigest()[:16], "soname": name}
+            break
+    return out
+
+
+def frame_golden(cfg, frame):
+    """The reference's whole-image hashes of `frame` at this configuration
+    (tests/golden/full_render_s1024.json, made by make_anim_golden.py full1024),
+    or None."""
+    path = os.path.join(ROOT, "tests", "golden", "full_render_s1024.json")
+    try:
+        g = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if (g["width"], g["height"], g["spp"]) != (cfg.width, cfg.height, cfg.samples_per_pixel) or cfg.max_bounces != 4:
+        return None
+    return g["frames"].get(str(frame))
+
+
+def image_hashes(acc, bgra):
+    """(radiance xyz f32 bits [H][W][3], BGRA [H][W][4]) hashes, as the reference
+    harness's anim_render computes them (tests/anim_check.py)."""
+    import hashlib
+    import numpy as np
+    rad = np.ascontiguousarray(np.asarray(acc, np.float32)[..., :3])
+    return {"sha_radiance": hashlib.sha256(rad.view(np.uint32).tobytes()).hexdigest()[:32],
+            "sha_bgra": hashlib.sha256(np.ascontiguousarray(bgra, np.uint8).tobytes()).hexdigest()[:32]}
+
+
 def spot_rects(frame, w, h):
     """Three 2x2 rectangles per animation frame (centre + two frame-dependent)."""
     a = (frame * 2654435761) & 0xFFFFFFFF
@@ -335,16 +393,31 @@ def main():
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    ranks = None
     if world > 1:
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # the communicator's own size and every rank's device identity, so the
+        # line proves how many distinct GPUs took part
+        import socket
+        props = torch.cuda.get_device_properties(local)
+        me = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": props.name,
+              "pci": "%s:%s:%s" % (getattr(props, "pci_domain_id", "?"), getattr(props, "pci_bus_id", "?"),
+                                   getattr(props, "pci_device_id", "?")),
+              "uuid": str(getattr(props, "uuid", ""))}
+        allp = [None] * dist.get_world_size()
+        dist.all_gather_object(allp, me)
+        ranks = {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "devices": allp,
+                 "distinct_gpus": len({(d["host"], d["pci"], d["uuid"]) for d in allp})}
 
     assets = os.path.join(ROOT, "assets")
     cfg = N.RenderConfig.make(args.width, args.height, args.spp, args.bounces)
     scene = N.Scene(assets, cfg)
     r = GpuRenderer(local)
+    # the arithmetic environment the bit-exact results rest on (ptg_arith_selftest)
+    selftest = r.selftest()
     stream = torch.cuda.current_stream(local)
     r.set_stream(stream)
     r.set_concurrency(args.concurrency)
@@ -356,11 +429,12 @@ def main():
     r.upload(scene, include_static=True)
     dev = torch.device("cuda", local)
     image = torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device=dev)
+    accum = torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device=dev)
     shard = D.TileShard(cfg, tw, th, rank, world) if args.shard == "tiles" else None
 
     def render_step():
         if shard is None:
-            r.render(cfg, out_bgra=image)
+            r.render(cfg, out_bgra=image, out_accum=accum)   # the radiance too: the last step is hashed
         else:
             D.render_and_gather(r, cfg, shard, image, stream=stream)
 
@@ -375,14 +449,18 @@ def main():
 
     long_steps = cfg.width * cfg.height * cfg.samples_per_pixel > 4e9
 
-    def reduce_max(v):
-        if world > 1:
-            t = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            v = float(t.item())
-        return v
+    def gather_floats(v):
+        """v of every rank, in rank order."""
+        if world == 1:
+            return [v]
+        t = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else dev)
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [float(x.item()) for x in out]
 
-    def timed(fn, timing, steps=None, warmup=None):
+    per_rank_s = {}
+
+    def timed(fn, timing, steps=None, warmup=None, tag=None):
         """K steps of fn between barrier + synchronize on both sides; max over ranks."""
         steps = args.steps if steps is None else steps
         for _ in range(args.warmup if warmup is None else warmup):
@@ -405,15 +483,175 @@ def main():
         el = time.perf_counter() - t0
         kb = r.kernel_busy() if timing else {}
         r.enable_timing(False)
-        return reduce_max(el), kb
+        ranks_el = gather_floats(el)
+        if tag:
+            per_rank_s[tag] = ranks_el
+        return max(ranks_el), kb
+
+    def frame_check(f):
+        """This rank's last rendered frame (accum + image) against the reference's
+        whole-image hashes of frame f at this configuration, if the golden holds it."""
+        if shard is not None:
+            return None
+        want = frame_golden(cfg, f)
+        if want is None:
+            return None
+        got = image_hashes(accum.cpu().numpy(), image.cpu().numpy())
+        return {"frame": f, "exact": got == want, "radiance": got["sha_radiance"] == want["sha_radiance"],
+                "bgra": got["sha_bgra"] == want["sha_bgra"],
+                "golden": "tests/golden/full_render_s1024.json (the reference's strict build, whole image)"}
+
+    def walk_levels(kind, workload, busy_ms, launches, iso_ms):
+        """The roofline levels of one walk kind (extend / shadow) from the committed
+        PMC profile of this workload, or the reason there are none."""
+        ent, src = pmc_profile(kind, workload, iso_ms)
+        hier = hierarchy_roofline(ent, iso_ms * 1e-3) if ent else None
+        if not hier:
+            return {"bound": None, "ms_per_launch_isolated": round(iso_ms, 4),
+                    "basis": "no committed PMC profile of this workload whose launch time agrees with this run's "
+                             "(%.3f ms)" % iso_ms}, None, None
+        live_s = busy_ms * 1e-3 / launches
+        top = hier["levels"][hier["bound"]]
+        out = {"bound": hier["bound"], "frac_live": round(top["seconds"] / live_s, 5),
+               "frac_isolated": round(hier["t_min_s"] / (iso_ms * 1e-3), 5),
+               "ms_per_launch_live": round(busy_ms / launches, 4), "ms_per_launch_isolated": round(iso_ms, 4),
+               "launches_per_step": launches, "source": src,
+               "levels": {k: {"frac_isolated": round(v["frac"], 4), "frac_live": round(v["seconds"] / live_s, 4)}
+                          for k, v in hier["levels"].items()}}
+        return out, (ent, src, hier, live_s), top
+
+    def measure_roofline(workload, kb, steps, elapsed_s):
+        """Roofline of the closest-hit walk (the dominant kernel) and the levels of
+        both walks, for the frame currently uploaded: `kb` = the timed steps'
+        kernel_busy record; then one counting pass and one isolated pass (every
+        kernel on one stream), both untimed."""
+        step_busy_ms = {k: v[0] for k, v in kb.items() if v[2]}
+        step_sum_ms = {k: v[1] for k, v in kb.items() if v[2]}
+        step_launches = {k: v[2] for k, v in kb.items() if v[2]}
+        if long_steps:
+            print("counting pass", file=sys.stderr, flush=True)
+        r.enable_counters(True)
+        if shard is None:
+            r.render(cfg, out_bgra=image)
+        else:
+            r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+        r.synchronize()
+        kc = r.kernel_counters()
+        ws = r.walk_stats()
+        r.enable_counters(False)
+        total = sum(kc[k] for k in kc)
+        per_step_samples = int(total[0])
+        # dominant kernel: the closest-hit BVH walk (k_wf_walk<closest>, "extend")
+        wb = walker_bytes(ws["extend"], kc["extend"])           # bytes its own loads and stores move per step
+        launches = step_launches["extend"] / steps
+        busy_ms = step_busy_ms["extend"] / steps                 # union of its launch intervals per step
+        # the same kernels with nothing beside them: one untimed render with every
+        # kernel on one stream (the timed steps run up to 4 kernels at once)
+        if long_steps:
+            print("isolated-walk pass", file=sys.stderr, flush=True)
+        r.set_concurrency(0)
+        r.enable_timing(True)
+        if shard is None:
+            r.render(cfg, out_bgra=image)
+        else:
+            r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+        r.synchronize()
+        kb_iso = r.kernel_busy()
+        r.enable_timing(False)
+        r.set_concurrency(args.concurrency)
+        iso = {k: kb_iso[k][1] / max(1, kb_iso[k][2]) for k in ("extend", "shadow")}
+        walks = {}
+        ext = None
+        for k in ("extend", "shadow"):
+            if step_launches.get(k):
+                walks[k], info, top = walk_levels(k, workload, step_busy_ms[k] / steps, step_launches[k] / steps,
+                                                  iso[k])
+                if k == "extend":
+                    ext = (info, top)
+        iso_ms = iso["extend"]
+        path_ms = elapsed_s / steps * 1e3
+        path_bytes = algorithmic_bytes(total)
+        w = ws["extend"]
+        lanes = {"node_phase": round(w["node_lanes"] / max(1, w["node_phases"]), 2),
+                 "leaf_phase": round(w["leaf_lanes"] / max(1, w["leaf_phases"]), 2),
+                 "refill": round(w["refill_lanes"] / max(1, w["refills"]), 2),
+                 "active_per_iteration": round(w["active_lanes"] / max(1, w["iterations"]), 2)}
+        wsh = ws["shadow"]
+        lanes_any = {"node_phase": round(wsh["node_lanes"] / max(1, wsh["node_phases"]), 2),
+                     "leaf_phase": round(wsh["leaf_lanes"] / max(1, wsh["leaf_phases"]), 2),
+                     "refill": round(wsh["refill_lanes"] / max(1, wsh["refills"]), 2),
+                     "active_per_iteration": round(wsh["active_lanes"] / max(1, wsh["iterations"]), 2)}
+        roof = {"kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)", "workload": workload}
+        if ext and ext[0]:
+            (ent, prof_src, hier, live_s), top = ext
+            roof.update({
+                "bound": hier["bound"],
+                # in the bound level's own unit: its count per launch over the
+                # live time per launch, against that level's measured ceiling
+                "achieved": round(top["count"] / live_s / 1e9, 3),
+                "peak": round(top["ceiling_per_s"] / 1e9, 3),
+                "unit": "G " + top["unit"] + " per s",
+                "frac": round(top["count"] / live_s / top["ceiling_per_s"], 5),
+                "traffic": int(ent["derived"]["hbm_side_bytes"]),
+                "traffic_source": "%s (rocprofv3 --pmc passes of this workload, per launch: FETCH_SIZE x 1 KiB "
+                                  "x 2 + WRITE_SIZE x 1 KiB)" % prof_src,
+                "basis": "bound = the memory/issue level with the largest time floor for one launch (count "
+                         "from the committed PMC profile of this workload / ceiling measured on MI355X for the "
+                         "walk's access shape, see 'levels'); achieved = that count / the launch's live time "
+                         "(busy time per step, union of its launch intervals on HIP events, / launches per "
+                         "step); frac = achieved / peak = floor / live time",
+                "levels": {k: {"count_per_launch": v["count"], "unit": v["unit"],
+                               "ceiling_per_s": v["ceiling_per_s"], "frac_isolated": round(v["frac"], 4),
+                               "frac_live": round(v["seconds"] / live_s, 4)} for k, v in hier["levels"].items()},
+                "ceilings_source": hier["ceilings_source"],
+                "hbm": {"bytes_per_launch": int(ent["derived"]["hbm_side_bytes"]),
+                        "achieved_GBps": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9, 2),
+                        "peak_GBps": HBM_PEAK_GBS,
+                        "frac": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9 / HBM_PEAK_GBS, 5)}})
+        else:
+            roof.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                         "traffic": None,
+                         "basis": "no committed PMC profile of this workload whose launch time agrees with "
+                                  "this run's (%.3f ms): levels not derived" % iso_ms})
+        roof.update({
+            "ms_per_launch": round(busy_ms / launches, 4), "launches_per_step": launches,
+            "isolated": {"ms_per_launch": round(iso_ms, 4),
+                         "frac": walks.get("extend", {}).get("frac_isolated"),
+                         "basis": "one extra untimed render with every kernel on one stream "
+                                  "(ptg_set_concurrency(0))"},
+            "walks": walks,
+            "walker_bytes": {"per_launch": int(wb / launches),
+                             "achieved_GBps": round(wb / (busy_ms * 1e-3) / 1e9, 2),
+                             "basis": "bytes the walk's own vector-memory instructions move (counting pass, "
+                                      "ptg_last_walk_stats): 7 x 16 B block rows per node-phase lane, 4 x 16 B "
+                                      "record rows per leaf-phase lane, 48 B of ray state per started ray, 32 B "
+                                      "of result per finished ray; mostly served by L2 and the Infinity Cache, "
+                                      "so it is compared with no HBM figure"},
+            "lanes_per_vmem_instruction": lanes,
+            "lanes_per_vmem_instruction_any_hit": lanes_any,
+            "kernel_busy_ms_per_step": {k: round(v / steps, 3) for k, v in step_busy_ms.items()},
+            "kernel_sum_ms_per_step": {k: round(v / steps, 3) for k, v in step_sum_ms.items()},
+            "reference_equivalent_bytes_rate": {
+                "GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
+                "bytes_per_sample": round(path_bytes / per_step_samples, 1),
+                "basis": "SURVEY 8(d)'s formula, 32 visits + 60 tri + 88 enter + 156 shade + 160 per sample: "
+                         "what the REFERENCE's stackless walk would read per sample, over the wall time per "
+                         "step.  Not a memory rate of this code (the block walker reads other records, mostly "
+                         "from cache) and not comparable with HBM peak"},
+            "per_sample": {"node_visits": round(total[1] / per_step_samples, 2),
+                           "triangle_tests": round(total[2] / per_step_samples, 2),
+                           "blas_entries": round(total[3] / per_step_samples, 2),
+                           "ray_queries": round(total[4] / per_step_samples, 3),
+                           "shades": round(total[5] / per_step_samples, 3)}})
+        return roof
+
+    def workload_of(f):
+        return "frame %d, %dx%d, %d spp, %d bounces" % (f, cfg.width, cfg.height, cfg.samples_per_pixel,
+                                                         cfg.max_bounces)
 
     # (1) the metric: render steps over a frame whose inputs are resident in HBM
-    elapsed, kb = timed(render_step, True)
-    # per-kernel device time of the K timed steps (HIP events on the launch streams):
-    # busy = union of a kind's launch intervals (overlapping launches counted once)
-    step_busy_ms = {k: v[0] for k, v in kb.items() if v[2]}
-    step_sum_ms = {k: v[1] for k, v in kb.items() if v[2]}
-    step_launches = {k: v[2] for k, v in kb.items() if v[2]}
+    elapsed, kb = timed(render_step, True, tag="metric")
+    main_check = frame_check(frame)   # this rank's last timed image against the reference's
     # (2) SURVEY 8(d)'s definition: W.H.SPP / (upload-frame + render + gather)
     elapsed_upload = None if args.no_frame_setup else timed(upload_step, False)[0]
     # (3) the reference's per-frame loop: host setup_animation_frame + PCIe upload + render
@@ -424,16 +662,19 @@ def main():
     value_upload = samples_per_step * args.steps / elapsed_upload / 1e6 if elapsed_upload else None
     value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
 
-    # (3) the heavy companion frame at the same configuration
+    # (3) the heavy companion frame at the same configuration, with its own roofline
     heavy = None
     if args.heavy_frame >= 0:
         hf = args.heavy_frame + (rank if args.shard == "frames" else 0)
         scene.setup_frame(hf)
         r.upload(scene, include_static=False)
         hsteps = max(1, min(args.steps, 3))
-        el_h, _ = timed(render_step, False, steps=hsteps, warmup=1)
+        el_h, kb_h = timed(render_step, True, steps=hsteps, warmup=1, tag="heavy_frame")
         heavy = {"frame": args.heavy_frame, "value": round(samples_per_step * hsteps / el_h / 1e6, 3),
-                 "unit": "Msamples/s", "ms_per_step": round(el_h / hsteps * 1e3, 3), "steps": hsteps}
+                 "unit": "Msamples/s", "ms_per_step": round(el_h / hsteps * 1e3, 3), "steps": hsteps,
+                 "frame_check": frame_check(hf)}
+        if rank == 0 and not args.no_roofline:
+            heavy["roofline"] = measure_roofline(workload_of(args.heavy_frame), kb_h, hsteps, el_h)
 
     # (4) the animation (BASELINE config 4): K frames spread evenly over all 1800 (frame
     # cost varies ~7x), frame-parallel over the ranks; each frame is set up on the host,
@@ -490,7 +731,9 @@ def main():
         writer.shutdown()
         if world > 1:
             dist.barrier()
-        anim_s = reduce_max(time.perf_counter() - t0)
+        anim_ranks = gather_floats(time.perf_counter() - t0)
+        per_rank_s["animation"] = anim_ranks
+        anim_s = max(anim_ranks)
         spots_out = args.spots_out or os.path.join(ROOT, "gpurun_out", "anim_spots_r%d.npz" % rank)
         os.makedirs(os.path.dirname(spots_out), exist_ok=True)
         np.savez_compressed(spots_out, frames=np.array(spots["frames"], np.int32),
@@ -513,8 +756,7 @@ def main():
                         "rectangles of every frame (radiance bits and BGRA) against the reference's own render of "
                         "them (tests/golden/bench_spots.npz, made by tests/golden/make_anim_golden.py)"}
 
-    workload = "frame %d, %dx%d, %d spp, %d bounces" % (args.frame, cfg.width, cfg.height, cfg.samples_per_pixel,
-                                                         cfg.max_bounces)
+    workload = workload_of(args.frame)
     result = None
     if rank == 0:
         roof = None
@@ -522,111 +764,7 @@ def main():
             if heavy is not None or anim is not None:   # back to the metric frame for the counting passes
                 scene.setup_frame(frame)
                 r.upload(scene, include_static=False)
-            # deterministic work counters and walk statistics of the same render
-            # (separate counting pass, untimed)
-            if long_steps:
-                print("counting pass", file=sys.stderr, flush=True)
-            r.enable_counters(True)
-            if shard is None:
-                r.render(cfg, out_bgra=image)
-            else:
-                r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
-            r.synchronize()
-            kc = r.kernel_counters()
-            ws = r.walk_stats()
-            r.enable_counters(False)
-            total = sum(kc[k] for k in kc)
-            per_step_samples = int(total[0])
-            # dominant kernel: the closest-hit BVH walk (k_wf_walk<closest>, "extend")
-            wb = walker_bytes(ws["extend"], kc["extend"])           # bytes its own loads and stores move per step
-            launches = step_launches["extend"] / args.steps
-            busy_ms = step_busy_ms["extend"] / args.steps            # union of its launch intervals per step
-            # the same kernel with nothing beside it: one untimed render with every
-            # kernel on one stream (the timed steps run up to 4 kernels at once)
-            if long_steps:
-                print("isolated-walk pass", file=sys.stderr, flush=True)
-            r.set_concurrency(0)
-            r.enable_timing(True)
-            if shard is None:
-                r.render(cfg, out_bgra=image)
-            else:
-                r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
-            r.synchronize()
-            kb_iso = r.kernel_busy()
-            r.enable_timing(False)
-            r.set_concurrency(args.concurrency)
-            iso_launches = max(1, kb_iso["extend"][2])
-            iso_ms = kb_iso["extend"][1] / iso_launches
-            ent, prof_src = pmc_profile("extend", workload, iso_ms)
-            hier = hierarchy_roofline(ent, iso_ms * 1e-3) if ent else None
-            path_ms = elapsed / args.steps * 1e3
-            path_bytes = algorithmic_bytes(total)
-            w = ws["extend"]
-            lanes = {"node_phase": round(w["node_lanes"] / max(1, w["node_phases"]), 2),
-                     "leaf_phase": round(w["leaf_lanes"] / max(1, w["leaf_phases"]), 2),
-                     "refill": round(w["refill_lanes"] / max(1, w["refills"]), 2),
-                     "active_per_iteration": round(w["active_lanes"] / max(1, w["iterations"]), 2)}
-            roof = {"kernel": "k_wf_walk<closest> (extend: closest-hit BVH walk)"}
-            if hier:
-                top = hier["levels"][hier["bound"]]
-                live_s = busy_ms * 1e-3 / launches                   # one launch's share of the live busy time
-                roof.update({
-                    "bound": hier["bound"],
-                    # in the bound level's own unit: its count per launch over the
-                    # live time per launch, against that level's measured ceiling
-                    "achieved": round(top["count"] / live_s / 1e9, 3),
-                    "peak": round(top["ceiling_per_s"] / 1e9, 3),
-                    "unit": "G " + top["unit"] + " per s",
-                    "frac": round(top["count"] / live_s / top["ceiling_per_s"], 5),
-                    "traffic": int(ent["derived"]["hbm_side_bytes"]),
-                    "traffic_source": "%s (rocprofv3 --pmc passes of this workload, per launch: FETCH_SIZE x 1 KiB "
-                                      "x 2 + WRITE_SIZE x 1 KiB)" % prof_src,
-                    "basis": "bound = the memory/issue level with the largest time floor for one launch (count "
-                             "from the committed PMC profile of this workload / ceiling measured on MI355X for the "
-                             "walk's access shape, see 'levels'); achieved = that count / the launch's live time "
-                             "(busy time per step, union of its launch intervals on HIP events, / launches per "
-                             "step); frac = achieved / peak = floor / live time",
-                    "levels": {k: {"count_per_launch": v["count"], "unit": v["unit"],
-                                   "ceiling_per_s": v["ceiling_per_s"], "frac_isolated": round(v["frac"], 4),
-                                   "frac_live": round(v["seconds"] / live_s, 4)} for k, v in hier["levels"].items()},
-                    "ceilings_source": hier["ceilings_source"],
-                    "hbm": {"bytes_per_launch": int(ent["derived"]["hbm_side_bytes"]),
-                            "achieved_GBps": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9, 2),
-                            "peak_GBps": HBM_PEAK_GBS,
-                            "frac": round(ent["derived"]["hbm_side_bytes"] / live_s / 1e9 / HBM_PEAK_GBS, 5)}})
-            else:
-                roof.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
-                             "traffic": None,
-                             "basis": "no committed PMC profile of this workload whose launch time agrees with "
-                                      "this run's (%.3f ms): levels not derived" % iso_ms})
-            roof.update({
-                "ms_per_launch": round(busy_ms / launches, 4), "launches_per_step": launches,
-                "isolated": {"ms_per_launch": round(iso_ms, 4),
-                             "frac": round(hier["t_min_s"] / (iso_ms * 1e-3), 5) if hier else None,
-                             "basis": "one extra untimed render with every kernel on one stream "
-                                      "(ptg_set_concurrency(0))"},
-                "walker_bytes": {"per_launch": int(wb / launches),
-                                 "achieved_GBps": round(wb / (busy_ms * 1e-3) / 1e9, 2),
-                                 "basis": "bytes the walk's own vector-memory instructions move (counting pass, "
-                                          "ptg_last_walk_stats): 7 x 16 B block rows per node-phase lane, 4 x 16 B "
-                                          "record rows per leaf-phase lane, 48 B of ray state per started ray, 32 B "
-                                          "of result per finished ray; mostly served by L2 and the Infinity Cache, "
-                                          "so it is compared with no HBM figure"},
-                "lanes_per_vmem_instruction": lanes,
-                "kernel_busy_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_busy_ms.items()},
-                "kernel_sum_ms_per_step": {k: round(v / args.steps, 3) for k, v in step_sum_ms.items()},
-                "reference_equivalent_bytes_rate": {
-                    "GBps": round(path_bytes / (path_ms * 1e-3) / 1e9, 2),
-                    "bytes_per_sample": round(path_bytes / per_step_samples, 1),
-                    "basis": "SURVEY 8(d)'s formula, 32 visits + 60 tri + 88 enter + 156 shade + 160 per sample: "
-                             "what the REFERENCE's stackless walk would read per sample, over the wall time per "
-                             "step.  Not a memory rate of this code (the block walker reads other records, mostly "
-                             "from cache) and not comparable with HBM peak"},
-                "per_sample": {"node_visits": round(total[1] / per_step_samples, 2),
-                               "triangle_tests": round(total[2] / per_step_samples, 2),
-                               "blas_entries": round(total[3] / per_step_samples, 2),
-                               "ray_queries": round(total[4] / per_step_samples, 3),
-                               "shades": round(total[5] / per_step_samples, 3)}})
+            roof = measure_roofline(workload, kb, args.steps, elapsed)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -638,7 +776,7 @@ def main():
             "metric": "Msamples/sec (whole node) at %dx%d %dspp" % (cfg.width, cfg.height, cfg.samples_per_pixel),
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": ranks["world_size"] if ranks else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -650,6 +788,12 @@ def main():
             "config": {"workload": workload + (" (BASELINE metric config)" if is_metric else ""),
                        "baseline_config": args.config,
                        "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
+            "frame_exact": None if main_check is None else main_check["exact"],
+            "frame_check": main_check,
+            "selftest": selftest,
+            "libm": libm_identity(),
+            "ranks": ranks,
+            "per_rank_seconds": {k: [round(x, 4) for x in v] for k, v in per_rank_s.items()} if world > 1 else None,
             "heavy_frame": heavy,
             "animation": anim,
             "value_survey_def": None if value_upload is None else {

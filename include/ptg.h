@@ -239,7 +239,9 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
  * kernels):
  * [0] samples, [1] node visits, [2] triangle tests, [3] BLAS entries,
  * [4] ray queries, [5] closest-hit shades, [6] TLAS node visits (part of [1]),
- * [7] walk-loop iterations of whole waves (diagnostics). */
+ * [7] walk-loop iterations of whole waves (diagnostics).  [5] counts shading
+ * passes: a surface path the certified pass lists for the exact pass
+ * (ptg_last_redo_stats out[0]) is counted twice. */
 int ptg_counters_enable(ptg_context* ctx, int enable);
 int ptg_last_counters(ptg_context* ctx, uint64_t out[8]);
 /* Counters split by kernel kind (same kinds as ptg_last_kernel_times). */
@@ -256,16 +258,27 @@ int ptg_last_kernel_counters(ptg_context* ctx, uint64_t out[6][8]);
 int ptg_last_walk_stats(ptg_context* ctx, uint64_t out[2][8]);
 
 /* The certified shading of the last ptg_render* call (counting builds, as
- * ptg_last_counters).  The wavefront pipeline's surface and sky kernels
- * evaluate the path's double-precision exp / pow / sin / cos with the GPU
- * library and prove per evaluation that the float the path keeps is the one
- * glibc's double gives (device/ref_math.h, float_certain); a path with an
- * evaluation the proof does not cover is shaded again with the restated
- * glibc algorithms.  out[0] / out[1]: surface / sky paths shaded again;
- * out[2..8]: per certificate site (acc_exp, exp_times, add_mul_pow,
+ * ptg_last_counters).  The wavefront pipeline's surface kernel evaluates
+ * the path's double-precision exp / pow / sin / cos with the GPU library and
+ * proves per evaluation that the float the path keeps is the one glibc's
+ * double gives (device/ref_math.h, float_certain); a path with an evaluation
+ * the proof does not cover is shaded again with the restated glibc
+ * algorithms.  The sky kernel runs the restated glibc algorithms directly
+ * and certifies nothing.  out[0]: surface paths shaded again; out[1]:
+ * reserved (always 0); out[2..8]: per certificate site (acc_exp, exp_times, add_mul_pow,
  * div_mul_pow, times_cos, times_sin, times_one_minus_div_pow) the paths in
  * which it failed. */
 int ptg_last_redo_stats(ptg_context* ctx, uint64_t out[9]);
+
+/* The arithmetic environment the bit-exact results rest on: the known-answer
+ * checks of ptg_device.h's ptg_device_selftest, compiled with this library's
+ * own flags and run on the context's device, against this host's libm.
+ * Returns the mask of failed checks (0: all passed; see ptg_device.h for the
+ * bits: FP contraction, glibc exp / pow / sin / cos, tonemap, fmin's tie rule,
+ * division), or a negative error code.  A nonzero mask means this host's
+ * reference build would not give the bits the GPU gives (a libm other than
+ * glibc 2.35's FMA variants), or the library was built with the wrong flags. */
+int ptg_arith_selftest(ptg_context* ctx);
 
 /* Per-launch device timing, measured with HIP events recorded around every
  * kernel launch on the context's stream.  Enabling (re)starts the record;

@@ -164,6 +164,9 @@ struct Io {
     float tie_out[2];
     float div_out[kArgs], rcp_out[kArgs];
 };
+/* internal linkage: several translation units of one library may include
+ * this header (tests/device_dropin builds a two-TU library to check it) */
+namespace {
 __global__ void kernel(Io* io)
 {
     if(threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -182,6 +185,7 @@ __global__ void kernel(Io* io)
     io->tie_out[0] = ptg::dm::gmin(io->c - io->c, -(io->c - io->c));   /* fmin(+0, -0): -0 */
     io->tie_out[1] = ptg::dm::gmax(-(io->c - io->c), io->c - io->c);   /* fmax(-0, +0): +0 */
 }
+} // namespace
 inline bool same(double a, double b) { return memcmp(&a, &b, sizeof a) == 0; }
 inline bool samef(float a, float b) { return memcmp(&a, &b, sizeof a) == 0; }
 } // namespace ptg_selftest

@@ -86,5 +86,8 @@ constexpr uint32_t kBeIndex = 0x0FFFFFFFu;   // 28-bit block indices and payload
 // payload); a leaf word sits on top of its `near` (float bits).  kBePop
 // (a leaf word no payload can produce) means "take the next stack entry".
 constexpr uint32_t kBePop = 0xFFFFFFFFu;
+// A parked triangle that is an any-hit walk's occluder candidate
+// (BlockWalker::try_candidate): its leaf box is tested from its vertices.
+constexpr uint32_t kBeCand = 0x20000000u;
 
 } // namespace ptg

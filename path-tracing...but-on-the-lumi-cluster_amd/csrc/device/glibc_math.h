@@ -26,6 +26,17 @@
 // Scope: exp on every double; pow on every x for the path's constant
 // exponents (a finite y with 2^-65 <= |y| < 2^63: 5, 0.25, 1.5, 1/2.4) -
 // glibc's y-special branch (y zero, inf, nan, tiny or huge) is not restated.
+//
+// Attribution and licence.  The algorithms and constant tables restated here
+// are those of the GNU C Library 2.35 (sysdeps/ieee754/dbl-64: e_exp.c,
+// e_pow.c, s_sin.c and their data files), which is licensed under the GNU
+// Lesser General Public License v2.1 or later.  glibc's exp and pow (and
+// their data) derive from Arm's optimized-routines (Szabolcs Nagy, Arm Ltd.,
+// MIT / Apache-2.0 WITH LLVM-exception upstream); sin / cos (s_sin.c,
+// __sincostab) are IBM Accurate Mathematical Library code contributed to
+// glibc.  This file restates those routines for the GPU so that its results
+// equal the host libm's bit for bit; the restated parts remain under their
+// original terms.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

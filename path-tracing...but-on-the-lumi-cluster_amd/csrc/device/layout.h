@@ -42,6 +42,23 @@ struct alignas(16) InstShade {
 };
 static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
 
+// InstBox 32 B: an instance's TLAS leaf box (the reference's leaf node, the
+// bounds of its transformed BLAS root box, bvh.cc:259-281) and where it is a
+// leaf: the any-hit walk's occluder candidates (k_wf_walk<ANY>) test an
+// instance's leaf box directly, without walking the TLAS down to it.
+//   lo.xyz, w = sub: the one subframe whose TLAS holds the instance, or
+//                    kInstAllSubframes (every TLAS holds it, with this same box),
+//                    or kInstNoCandidate (neither: never a candidate)
+//   hi.xyz, w = the triangle count of its mesh (candidate triangles are below it)
+struct alignas(16) InstBox {
+    float lo[3];
+    uint32_t sub;
+    float hi[3];
+    uint32_t tri_count;
+};
+static_assert(sizeof(InstBox) == 32, "InstBox is two 16-byte loads");
+constexpr uint32_t kInstAllSubframes = 0xFFFFFFFFu, kInstNoCandidate = 0xFFFFFFFEu;
+
 // Everything a hot-path kernel reads, passed by value as a kernel argument.
 struct DevScene {
     const BlockCopy* blocks;       // block BVH records of both levels (block_format.h), 8 copies per block
@@ -49,6 +66,7 @@ struct DevScene {
     const TriRec* tris;
     const InstTrav* inst_trav;
     const InstShade* inst_shade;
+    const InstBox* inst_box;       // per instance: TLAS leaf box + membership (occluder candidates)
     const uint32_t* indices;
     const float* normal;           // reference float3[] (16 B stride)
     const float* albedo;           // float4[]

@@ -137,6 +137,11 @@ struct RegCold {
     }
     PTG_D f3 world_o() const { return o; }
     PTG_D f3 world_d() const { return d; }
+    // any-hit occluder candidates are tried only by the wavefront walk (LdsCold)
+    PTG_D uint32_t candidate_skip() const { return 0xFFFFFFFFu; }
+    PTG_D uint32_t candidate_root() const { return kBePop; }
+    PTG_D void set_candidate(uint32_t, uint32_t) {}
+    PTG_D void clear_candidate_root() {}
     // ray_query_confirm (ray_query.hh:280-290)
     PTG_D void confirm(float u, float v, float t, uint32_t instance, uint32_t prim, bool back)
     {
@@ -152,8 +157,8 @@ struct RegCold {
 };
 
 struct WalkCold {              // one lane's LDS slot: two b128 accesses
-    float4 o;                  // world origin xyz
-    float4 d;                  // world direction xyz
+    float4 o;                  // world origin xyz; w: the any-hit candidate's instance (BlockWalker::try_candidate)
+    float4 d;                  // world direction xyz; w: the TLAS root still to walk after it, or kBePop
 };
 // LDS (address space 3) pointers to clang vector types: accesses through
 // them are ds_* instructions, never flat ones the compiler would have to
@@ -172,11 +177,26 @@ struct LdsCold {
 
     PTG_D void init(f3 ro, f3 rd, f3)
     {
-        c[0] = lds_f4v{ro.x, ro.y, ro.z, 0.0f};
-        c[1] = lds_f4v{rd.x, rd.y, rd.z, 0.0f};
+        c[0] = lds_f4v{ro.x, ro.y, ro.z, __uint_as_float(0xFFFFFFFFu)};
+        c[1] = lds_f4v{rd.x, rd.y, rd.z, __uint_as_float(kBePop)};
         bu = bv = 0.0f;
         binst = 0xFFFFFFFFu;
         bprim = 0;
+    }
+    // the any-hit candidate state sits in the w words of the world ray's rows,
+    // read with them at BLAS entry and exit (no registers held across steps)
+    PTG_D uint32_t candidate_skip() const { const lds_f4v v = c[0]; return __float_as_uint(v.w); }
+    PTG_D uint32_t candidate_root() const { const lds_f4v v = c[1]; return __float_as_uint(v.w); }
+    PTG_D void set_candidate(uint32_t inst, uint32_t root)
+    {
+        typedef __attribute__((address_space(3))) float lds_f_t;
+        reinterpret_cast<lds_f_t*>(c)[3] = __uint_as_float(inst);
+        reinterpret_cast<lds_f_t*>(c)[7] = __uint_as_float(root);
+    }
+    PTG_D void clear_candidate_root()
+    {
+        typedef __attribute__((address_space(3))) float lds_f_t;
+        reinterpret_cast<lds_f_t*>(c)[7] = __uint_as_float(kBePop);
     }
     PTG_D f3 world_o() const { const lds_f4v v = c[0]; return V3(v.x, v.y, v.z); }
     PTG_D f3 world_d() const { const lds_f4v v = c[1]; return V3(v.x, v.y, v.z); }
@@ -341,6 +361,51 @@ struct BlockWalker {
         pend = kBePop;
         pnear = 0.0f;
     }
+
+    // Any hit only (trace_shadow_ray, path_tracer.hh:415-427): the walk returns
+    // whether ANY triangle passes its TLAS leaf box, its BLAS leaf box and its
+    // triangle test - tmax never shrinks (no ray_query_confirm), so by
+    // containment (block_format.h) the ancestors pass too, and the order in
+    // which leaves are met does not change the result.  A candidate (instance
+    // ci, triangle cp of its mesh - where a nearby ray found its occluder) is
+    // therefore met first: ci's TLAS leaf box is tested here against its
+    // InstBox (the reference's leaf node; ci must be a leaf of this ray's
+    // subframe's TLAS), its BLAS is entered and walked whole with cp parked
+    // first (cp's leaf box, its vertex bounds, tested with the triangle), and
+    // then the TLAS from its root with ci's leaf skipped (ci held no
+    // occluder).  Call right after init().  The instance to skip and the TLAS
+    // root still to walk live in the cold state (Cold::set_candidate), the
+    // candidate triangle in pend (flag kBeCand; a parked triangle waits for
+    // the BLAS entry, leaf_select).  A walk that returns 2 leaves the
+    // occluding triangle in cur.
+    PTG_D void try_candidate(const DevScene& sc, uint32_t ci, uint32_t cp, uint32_t sub)
+    {
+        if(ci >= sc.inst_count || cur == kBePop) return;
+        const float4* b = reinterpret_cast<const float4*>(sc.inst_box + ci);
+        const float4 lo = b[0], hi = b[1];
+        const uint32_t in = __float_as_uint(lo.w);
+        float nv;
+        if((in != sub && in != kInstAllSubframes) || cp >= __float_as_uint(hi.w) || !box(lo, hi, nv)) return;
+        cold.set_candidate(ci, cur);
+        cur = kBeLeaf | ci;
+        cnear = nv;
+        pend = kBeLeaf | kBeCand | cp;
+        pnear = -__builtin_inff();
+    }
+    // When a walk with a candidate ends (node step returned 1: the stack is
+    // empty and the walk is back at the TLAS level), the candidate's instance
+    // has been walked whole without an occluder: the walk goes on over the
+    // TLAS from its root, skipping that instance's leaf.  Returns whether it
+    // goes on.
+    PTG_D bool resume_tlas()
+    {
+        const uint32_t root = cold.candidate_root();
+        if(root == kBePop) return false;
+        cur = root;
+        cnear = -__builtin_inff();
+        cold.clear_candidate_root();
+        return true;
+    }
     PTG_D Hit result() const { return cold.result(tmax); }
 
     // slab test (ray_query.hh:197-207) with its entry distance
@@ -416,7 +481,11 @@ struct BlockWalker {
         if(tri_accept(org, axis, S, V3(q0.x, q0.y, q0.z), V3(q0.w, q1.x, q1.y), V3(q1.z, q1.w, q2.x), tmin, tmax, u, v, t,
                       back))
         {
-            if(ANY) return 2;
+            if(ANY)
+            {
+                cur = leaf;   // the occluder, for the caller (the walk has ended)
+                return 2;
+            }
             cold.confirm(u, v, t, inst, leaf, back);
             tmax = t;
         }
@@ -464,7 +533,7 @@ struct BlockWalker {
             inv = winv;
             fin = finite3(winv);
             oct = octant(cold.world_d());
-            if(st.size() == 0) return 1;
+            if(st.size() == 0) return 1;   // (ANY: resume_tlas may go on)
         }
         const uint2 e = st.pop();
         const float n = __uint_as_float(e.y);
@@ -594,12 +663,16 @@ struct BlockWalker {
     struct LeafSel {
         const v4f* p;
         uint32_t id;
-        bool parked, inst_leaf, tri;
+        bool parked, inst_leaf, tri, cand;
     };
+    template<bool ANY = false>
     PTG_D LeafSel leaf_select(const DevScene& sc)
     {
         LeafSel ls;
-        ls.parked = pend != kBePop;
+        // (ANY: a candidate triangle is parked before its instance is entered,
+        // try_candidate; it waits until the walk is in that BLAS)
+        ls.parked = pend != kBePop && (!ANY || axis >= 0);
+        ls.cand = ls.parked && (pend & kBeCand) != 0;   // a candidate triangle: its leaf box is still to test
         ls.id = (ls.parked ? pend : cur) & kBeIndex;
         const float n = ls.parked ? pnear : cnear;
         if(ls.parked) pend = kBePop;
@@ -626,10 +699,23 @@ struct BlockWalker {
         }
         if(ls.inst_leaf)
         {
+            // the TLAS walk after a candidate's instance (try_candidate) skips it
+            if(ANY && ls.id == cold.candidate_skip() && cold.candidate_root() == kBePop) return 0;
             enter(ls.id, r0, r1, r2, r3);
             return 0;
         }
-        if(ls.tri)
+        bool in_box = true;
+        if(ANY && ls.cand)
+        {   // a candidate's BLAS leaf box: its vertex bounds (bvh.cc:243-246: fmin / fmax
+            // of the three positions; the upload checked every leaf box of this BLAS is)
+            const float4 lo = make_float4(gmin(r0.x, gmin(r0.w, r1.z)), gmin(r0.y, gmin(r1.x, r1.w)),
+                                          gmin(r0.z, gmin(r1.y, r2.x)), 0.0f);
+            const float4 hi = make_float4(gmax(r0.x, gmax(r0.w, r1.z)), gmax(r0.y, gmax(r1.x, r1.w)),
+                                          gmax(r0.z, gmax(r1.y, r2.x)), 0.0f);
+            float nv;
+            in_box = box(lo, hi, nv);
+        }
+        if(ls.tri && in_box)
             if(const int r = tri_test<ANY>(ls.id, make_float4(r0.x, r0.y, r0.z, r0.w), make_float4(r1.x, r1.y, r1.z, r1.w),
                                            make_float4(r2.x, r2.y, r2.z, r2.w)))
                 return r;
@@ -646,7 +732,7 @@ struct BlockWalker {
     template<bool ANY, bool COUNT>
     PTG_D int leaf_step(const DevScene& sc, Counters& cnt)
     {
-        const LeafSel ls = leaf_select(sc);
+        const LeafSel ls = leaf_select<ANY>(sc);
         if(ls.inst_leaf) PTG_CHECK(sc, ls.id < sc.inst_count, kDebugInst);
         if(!ls.inst_leaf) PTG_CHECK(sc, tri_base + ls.id < sc.tri_count, kDebugTri);   // read even when culled
         // every leaf lane reads its record, also a triangle whose deferred

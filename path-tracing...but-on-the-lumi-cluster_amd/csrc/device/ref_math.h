@@ -210,11 +210,16 @@ struct MathExactLds : MathExact {   // the same, exp's table copied to LDS by th
     glibc::ExpTabLds xt;
     PTG_D double exp(double x) const { return glibc::exp(x, xt); }
 };
+// PTG_CERT_FAIL_ALL=1 (test build libptg_certfail.so only): every certificate
+// fails, so every surface path takes the exact redo pass
+#ifndef PTG_CERT_FAIL_ALL
+#define PTG_CERT_FAIL_ALL 0
+#endif
 struct MathFast {    // ocml's, certified; fail_mask: bit CS_x when a certificate at site x did not hold
     static constexpr bool kFast = true;
     static constexpr bool kLdsExp = false;
     uint32_t fail_mask = 0;
-    PTG_D void check(bool certain, double, int site) { fail_mask |= certain ? 0u : 1u << site; }
+    PTG_D void check(bool certain, double, int site) { fail_mask |= (certain && !PTG_CERT_FAIL_ALL) ? 0u : 1u << site; }
 };
 
 // Arguments where both libraries return the exact value, so the double is

@@ -18,11 +18,14 @@
 #include "device/layout.h"
 #include "device/path_tracer.h"
 #include "device/wavefront.h"
+#include "ptg_device.h"   // ptg_device_selftest, compiled here with the library's own flags (ptg_arith_selftest)
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <tuple>
 #include <string>
 #include <vector>
 #include <unordered_map>
@@ -233,6 +236,10 @@ constexpr uint32_t kBands = 1024;   // XCD bands of a walk queue: a multiple of 
 // a chunk's device counters: per round the queue / NEE list lengths (2 words,
 // plus 4 spare), the hit / sky list lengths (2), the redo list lengths (2)
 constexpr uint32_t kCountWords(uint32_t rounds) { return 4 * (rounds + 2) + 2 * rounds; }
+// a chunk pipeline's state bytes per queued path, as render_map carves them:
+// 2 ping-pong PathSoA halves of 9 x 16 B, 2 TraceOut sets (hit 16 B, bary
+// 16 B, shadow 4 B), 5 lists of 4 B (2 NEE lists, hit, sky, redo)
+constexpr size_t kStateBytesPerPath = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 5 * 4;
 constexpr uint32_t kRedoGrid = 16;   // blocks of the MathExact shading passes (grid-stride over a short list)
 
 // Walk statistics of the counting build (per walk kind, see WalkStats): how
@@ -277,6 +284,11 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
     bool active = false;
     uint32_t q = 0;
+    // ANY: the wave's latest occluder (instance, triangle), wave-uniform (in
+    // scalar registers): the candidate its next rays try first
+    // (BlockWalker::try_candidate; a wave's rays come from one 8-pixel x
+    // 8-sample group at a time, their shadow rays are nearly parallel)
+    uint32_t occ_inst = 0xFFFFFFFFu, occ_prim = 0;
     // a finished walk writes its result: the shadow flag, or the closest hit;
     // results stream once through the caches (non-temporal), so they do not
     // evict BVH records from L2 / the Infinity Cache
@@ -327,6 +339,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                             const uint4 m = nt_load(S.meta + q);
                             w.init(m.z, xyz(nt_load(S.ray_o + q)),
                                    ANY ? xyz(nt_load(S.nee_d + q)) : xyz(nt_load(S.ray_d + q)), tmin, tmax);
+                            if(ANY) w.try_candidate(sc, occ_inst, occ_prim, meta_sub(m));
                             active = true;
                             took = true;
                             if(COUNT) cnt.queries++;
@@ -359,13 +372,33 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             if(COUNT) cnt.step_loads = 0;
             if(active && !w.at_leaf()) r = w.template node_step<COUNT>(sc, cnt);   // (a lane with a parked triangle walks on)
             if(COUNT) tally(WS_NODE_WAVES, (cnt.step_loads & 1u) != 0);
-            if(active && r != 0) { finish(r); active = false; r = 0; }
+            if(active && r != 0)
+            {   // ANY: after a candidate's instance, the TLAS (BlockWalker::resume_tlas)
+                if(!(ANY && w.resume_tlas()))
+                {
+                    finish(r);
+                    active = false;
+                }
+                r = 0;
+            }
         }
         if(COUNT) cnt.step_loads = 0;
+        bool occluded = false;
         if(active && w.wants_leaf())
         {
             r = w.template leaf_step<ANY, COUNT>(sc, cnt);
+            occluded = ANY && r == 2;
             if(r != 0) { finish(r); active = false; }
+        }
+        if(ANY)
+        {   // the wave's candidate becomes an occluder one of its lanes just found
+            const unsigned long long om = __ballot(occluded);
+            if(om)
+            {
+                const int l = __ffsll((long long)om) - 1;
+                occ_inst = __builtin_amdgcn_readlane(w.inst, l);
+                occ_prim = __builtin_amdgcn_readlane(w.cur, l);   // a walk that returned 2 left its occluder in cur
+            }
         }
         if(COUNT) tally(WS_LEAF_WAVES, (cnt.step_loads & 6u) != 0);
     }
@@ -784,6 +817,12 @@ struct ptg_context {
     DevBuf indices, pos, normal, albedo, material, tris;
     std::vector<ptg_bvh_node> host_nodes;
     std::vector<ptg_bvh_link> host_links;
+    std::vector<uint32_t> host_indices;    // the mesh arrays the occluder candidates' leaf boxes are checked against
+    std::vector<ptg_float3> host_pos;
+    // per (BLAS, mesh): every BLAS leaf's box is its triangle's vertex bounds
+    // (bvh.cc:243-246), so a candidate triangle's leaf box can be computed from
+    // its vertices (k_wf_walk<ANY>); checked once per pair on the host
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, bool> leaf_bounds_ok;
     size_t static_nodes = 0, index_count = 0, vertex_count = 0;
     std::unordered_set<uint32_t> packed_mesh;
     // BLAS blocks packed so far (host copy; their device copy leads `blocks`)
@@ -791,7 +830,7 @@ struct ptg_context {
     size_t blas_on_device = 0;                           // leading cache.blas entries already in `blocks`
     bool scene_ready = false;
     // frame: blocks = [BLAS blocks][this frame's TLAS blocks]
-    DevBuf blocks, tlas_root, subframes, inst_trav, inst_shade, jobs, polygon, spill;
+    DevBuf blocks, tlas_root, subframes, inst_trav, inst_shade, inst_box, jobs, polygon, spill;
     HostStage stage[2];                                  // ptg_upload_frame's pinned staging, used alternately
     uint32_t stage_next = 0;
     size_t block_count = 0, subframe_count = 0, instance_count = 0;
@@ -815,8 +854,8 @@ struct ptg_context {
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
     uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (ptg_set_hbm_share)
-    // wavefront: <= 2^chunk_log2 live paths per chunk.  2^27 paths x 392 B =
-    // 53 GB per pipeline, ~37% of an MI355X's HBM for the two pipelines
+    // wavefront: <= 2^chunk_log2 live paths per chunk.  2^27 paths x 396 B
+    // (kStateBytesPerPath + the 16 B sample) = 53 GB per pipeline, ~37% of an MI355X's HBM for the two pipelines
     // together, so a default render leaves most of the GPU to other tenants;
     // 2^28 (73%) is 1-3% faster on a GPU the renderer owns alone.
     uint32_t chunk_log2 = 27;
@@ -902,6 +941,7 @@ struct ptg_context {
         s.tris = tris.as<TriRec>();
         s.inst_trav = inst_trav.as<InstTrav>();
         s.inst_shade = inst_shade.as<InstShade>();
+        s.inst_box = inst_box.as<InstBox>();
         s.indices = indices.as<uint32_t>();
         s.normal = normal.as<float>();
         s.albedo = albedo.as<float>();
@@ -999,7 +1039,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     {
         size_t free_b = 0, total_b = 0;
         PTG_HIP(hipMemGetInfo(&free_b, &total_b));
-        const size_t per_path = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 4 * 4 + sizeof(float4);
+        const size_t per_path = kStateBytesPerPath + sizeof(float4);   // + the path's per-sample result
         // a slot's share of HBM, but never more than what is actually free (other
         // tenants, torch's cache): buffers this context already holds count as free
         size_t held = 0;
@@ -1042,7 +1082,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         for(uint32_t k = 0; k < nslots; ++k)
         {
             const size_t rec = M * 16;
-            PTG_HIP(ctx->grow(*slots[k].state, 2 * 9 * rec + 2 * M * (16 + 16 + 4) + 5 * M * 4 + kCountWords(rounds) * 4 + 256));
+            PTG_HIP(ctx->grow(*slots[k].state, M * kStateBytesPerPath + kCountWords(rounds) * 4 + 256));
             char* b = slots[k].state->as<char>();
             SlotState& t = st[k];
             for(int h = 0; h < 2; ++h)
@@ -1427,6 +1467,9 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     {   // the BLASes are packed into blocks on the host when an instance first names them
         ctx->host_nodes.assign(nodes, nodes + node_count);
         ctx->host_links.assign(links, links + 8 * node_count);
+        ctx->host_indices.assign(indices, indices + index_count);
+        ctx->host_pos.assign(pos, pos + vertex_count);
+        ctx->leaf_bounds_ok.clear();
     }
     catch(const std::bad_alloc&)
     {
@@ -1505,6 +1548,77 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
             mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
     }
 
+    // Per instance its TLAS leaf box and the subframes whose TLAS holds it
+    // (InstBox, the any-hit walk's occluder candidates): read from the
+    // reference-layout TLAS nodes (octant 0's links name the leaves).  A static
+    // instance is a leaf of every subframe's TLAS with the same box (computed
+    // from its transform alone, bvh.cc:259-281); a dynamic one of exactly one.
+    // Anything else is never a candidate.
+    // A candidate triangle's BLAS leaf box is computed from its vertices: the
+    // instance offers triangle candidates (tri_count > 0) only if every leaf
+    // box of its BLAS is exactly its triangle's bounds (checked once per pair).
+    auto leaf_bounds_ok = [&](const ptg_tlas_instance& in) {
+        const auto key = std::make_tuple(in.blas.node_offset, in.m.index_offset, in.m.base_vertex_offset);
+        auto it = ctx->leaf_bounds_ok.find(key);
+        if(it != ctx->leaf_bounds_ok.end()) return it->second;
+        bool ok = true;
+        for(uint32_t n = 0; ok && n < in.blas.node_count; ++n)
+        {
+            const ptg_bvh_link& l = ctx->host_links[size_t(in.blas.node_offset) * 8 + n];   // octant 0's order
+            if(!(l.accept & 0x80000000u)) continue;
+            const uint32_t t = l.accept & 0x7FFFFFFFu;
+            const size_t i0 = size_t(in.m.index_offset) + 3 * size_t(t);
+            if(t >= in.m.triangle_count || i0 + 2 >= ctx->host_indices.size()) { ok = false; break; }
+            float lo[3], hi[3];
+            const ptg_float3* P[3];
+            for(int k = 0; k < 3; ++k)
+            {
+                const size_t v = size_t(in.m.base_vertex_offset) + ctx->host_indices[i0 + k];
+                if(v >= ctx->host_pos.size()) { ok = false; break; }
+                P[k] = &ctx->host_pos[v];
+            }
+            if(!ok) break;
+            lo[0] = std::fmin(P[0]->x, std::fmin(P[1]->x, P[2]->x));
+            lo[1] = std::fmin(P[0]->y, std::fmin(P[1]->y, P[2]->y));
+            lo[2] = std::fmin(P[0]->z, std::fmin(P[1]->z, P[2]->z));
+            hi[0] = std::fmax(P[0]->x, std::fmax(P[1]->x, P[2]->x));
+            hi[1] = std::fmax(P[0]->y, std::fmax(P[1]->y, P[2]->y));
+            hi[2] = std::fmax(P[0]->z, std::fmax(P[1]->z, P[2]->z));
+            const ptg_bvh_node& nd = ctx->host_nodes[size_t(in.blas.node_offset) + n];
+            ok = memcmp(lo, &nd.min_x, 12) == 0 && memcmp(hi, &nd.max_x, 12) == 0;
+        }
+        ctx->leaf_bounds_ok[key] = ok;
+        return ok;
+    };
+    std::vector<InstBox> ib(instance_count);
+    {
+        std::vector<uint32_t> seen(instance_count, 0);
+        for(size_t i = 0; i < instance_count; ++i)
+        {
+            const uint32_t tris = leaf_bounds_ok(instances[i]) ? instances[i].m.triangle_count : 0u;
+            ib[i] = InstBox{{0, 0, 0}, kInstNoCandidate, {0, 0, 0}, tris};
+        }
+        for(size_t sf = 0; sf < subframe_count; ++sf)
+        {
+            const ptg_bvh tl = subframes[sf].tlas;   // ranges validated by pack_frame
+            const size_t base = size_t(tl.node_offset) - first_node;
+            for(uint32_t n = 0; n < tl.node_count; ++n)
+            {
+                const ptg_bvh_link& l = frame_links[8 * base + n];
+                if(!(l.accept & 0x80000000u)) continue;
+                const uint32_t i = l.accept & 0x7FFFFFFFu;
+                if(i >= instance_count) continue;
+                const ptg_bvh_node& nd = frame_nodes[base + n];
+                const InstBox b{{nd.min_x, nd.min_y, nd.min_z}, uint32_t(sf), {nd.max_x, nd.max_y, nd.max_z}, ib[i].tri_count};
+                if(seen[i]++ == 0) ib[i] = b;
+                else if(memcmp(ib[i].lo, b.lo, 12) != 0 || memcmp(ib[i].hi, b.hi, 12) != 0) ib[i].sub = kInstNoCandidate;
+            }
+        }
+        for(size_t i = 0; i < instance_count; ++i)
+            if(seen[i] > 1 && ib[i].sub != kInstNoCandidate)
+                ib[i].sub = seen[i] == subframe_count ? kInstAllSubframes : kInstNoCandidate;
+    }
+
     // Device copies, asynchronous: everything the frame uploads is gathered
     // into one of two pinned staging buffers and copied on the context's
     // stream, behind the render already queued there - the host returns at
@@ -1528,6 +1642,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     PTG_HIP(grow(ctx->tlas_root, subframe_count * sizeof(uint32_t)));
     PTG_HIP(grow(ctx->inst_trav, instance_count * sizeof(InstTrav)));
     PTG_HIP(grow(ctx->inst_shade, instance_count * sizeof(InstShade)));
+    PTG_HIP(grow(ctx->inst_box, instance_count * sizeof(InstBox)));
     PTG_HIP(grow(ctx->subframes, subframe_count * sizeof(ptg_subframe)));
     PTG_HIP(grow(ctx->polygon, subframe_count * kPolyStride * sizeof(float2)));
     if(!mesh_jobs.empty()) PTG_HIP(grow(ctx->jobs, mesh_jobs.size() * sizeof(MeshJob)));
@@ -1542,6 +1657,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     parts.push_back({fp.tlas_root.data(), subframe_count * sizeof(uint32_t), ctx->tlas_root.p});
     parts.push_back({it.data(), instance_count * sizeof(InstTrav), ctx->inst_trav.p});
     parts.push_back({is.data(), instance_count * sizeof(InstShade), ctx->inst_shade.p});
+    parts.push_back({ib.data(), instance_count * sizeof(InstBox), ctx->inst_box.p});
     parts.push_back({subframes, subframe_count * sizeof(ptg_subframe), ctx->subframes.p});
     parts.push_back({mesh_jobs.data(), mesh_jobs.size() * sizeof(MeshJob), ctx->jobs.p});
     size_t total = 0;
@@ -1883,6 +1999,14 @@ int ptg_set_pipeline(ptg_context* ctx, int pipeline)
     if(!ctx || pipeline < 0 || pipeline > 1) return fail(PTG_E_INVALID, "ptg_set_pipeline: 0 = wavefront, 1 = megakernel");
     ctx->pipeline = pipeline;
     return PTG_OK;
+}
+
+int ptg_arith_selftest(ptg_context* ctx)
+{
+    if(int r = bind(ctx)) return r;
+    const int m = ptg_device_selftest(ctx->stream);
+    if(m < 0) return fail(PTG_E_HIP, std::string("ptg_arith_selftest: ") + hipGetErrorString(hipError_t(-m)));
+    return m;
 }
 
 int ptg_synchronize(ptg_context* ctx)

@@ -107,10 +107,13 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
     The collective runs when the shard describes this process's place in the
     default process group (shard.world == group size, shard.rank == group
     rank; at world size 1 too, with `force_collective`).  A one-rank shard
-    (shard.world == 1) in a larger job, or with no group, is rendered locally;
-    any other mismatch raises before anything is rendered, so no rank waits in
-    a collective the others never join.  Over gloo (CPU groups: tests,
-    rehearsals) the tiles go through host memory.
+    (shard.world == 1) in a larger job, or with no group, is rendered locally.
+    Any other mismatch raises on the rank that has it, before that rank
+    renders.  The check is local: a rank whose own shard matches still enters
+    the gather, which then fails only when the mismatched rank's process exits
+    (or at the group's timeout).  Build every rank's shard from the same
+    (cfg, tile size, world size).  Over gloo (CPU groups: tests, rehearsals)
+    the tiles go through host memory.
     """
     import contextlib
 

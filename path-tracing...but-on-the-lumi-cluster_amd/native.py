@@ -91,6 +91,7 @@ def lib():
     P, U32, SZ, I = C.c_void_p, C.c_uint32, C.c_size_t, C.c_int
     sig = {
         "ptg_abi_version": (I, []),
+        "ptg_arith_selftest": (I, [P]),
         "ptg_last_error": (C.c_char_p, []),
         "ptg_set_host_threads": (I, [I]),
         "ptg_render_config_default": (None, [P]),

@@ -204,6 +204,14 @@ class GpuRenderer:
                  "times_one_minus_div_pow")
         return {"surface": int(out[0]), "sky": int(out[1]), "sites": {n: int(out[2 + k]) for k, n in enumerate(names)}}
 
+    def selftest(self):
+        """ptg_arith_selftest: mask of the failed arithmetic known-answer checks (0 = all
+        passed) of the library's own build on this device against this host's libm."""
+        m = N.lib().ptg_arith_selftest(self._ctx)
+        if m < 0:
+            N.check(m, "ptg_arith_selftest")
+        return int(m)
+
     def set_concurrency(self, level):
         """0: one stream; 1: sky/shadow kernels on a second stream; 2 (default):
         also two sample chunks in flight.  Identical bits at every level."""

@@ -136,3 +136,36 @@ def test_device_selftest_flags_contraction(native_lib):
     L.user_selftest.restype = C.c_int
     r = L.user_selftest()
     assert r > 0 and (r & 1), r
+
+
+LIB_2TU = os.path.join(ROOT, "tests", "device_dropin", "_build", "libuser_kernel_2tu.so")
+
+
+def test_two_translation_units_link():
+    """A user library whose two .hip files both include ptg_device.h links
+    (the header's definitions are inline or internal), and exports both TUs'
+    entry points (no GPU work)."""
+    assert os.path.exists(LIB_2TU), "build it first: __graft_entry__.build() (tests/device_dropin/Makefile)"
+    L = C.CDLL(LIB_2TU)
+    for sym in ("user_selftest", "user_selftest_tu2", "user_tonemap_device", "user_tonemap_device_tu2"):
+        assert hasattr(L, sym), sym
+
+
+@pytest.mark.gpu
+def test_two_translation_units_selftest_and_tonemap():
+    """Both translation units' copies of the header run: each self-test passes
+    and each TU's tonemap_pixel kernel gives the reference's bytes."""
+    import torch
+    L = C.CDLL(LIB_2TU)
+    L.user_selftest.restype = C.c_int
+    L.user_selftest_tu2.restype = C.c_int
+    assert L.user_selftest() == 0
+    assert L.user_selftest_tu2() == 0
+    g = np.load(os.path.join(GOLDEN, "tonemap.npz"))
+    colors = torch.from_numpy(np.ascontiguousarray(g["colors"], np.float32)).to("cuda:0")
+    for fn in (L.user_tonemap_device, L.user_tonemap_device_tu2):
+        fn.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p]
+        fn.restype = C.c_int
+        out = torch.zeros((len(colors), 4), dtype=torch.uint8, device="cuda:0")
+        assert fn(len(colors), C.c_void_p(colors.data_ptr()), C.c_void_p(out.data_ptr())) == 0
+        assert np.array_equal(out.cpu().numpy(), g["bgra"])

@@ -203,19 +203,36 @@ def test_failed_frame_upload_leaves_no_stale_records(gpu, assets_dir):
 def test_config4_full_4096spp_spot_rects_bit_exact(gpu, assets_dir):
     """BASELINE configs[4] at its full size: 3840x2160, 4096 spp (512
     subframes), frame 690 with the dragon and the buddha in view - the render
-    the bench times (~70 s), spot rectangles bit-exact against the oracle."""
+    the bench times (~70 s).  The frame's scene arrays equal the reference's
+    (anim_scene_s4096_4k.json), and the spot rectangles equal, bit for bit,
+    both the reference's own render of them (config4_spots.npz, the strict
+    reference build at this configuration) and the oracle's."""
+    import json
+    from anim_check import scene_frame_hashes
     w, h, spp, frame = 3840, 2160, 4096, 690
     s = scene_for(assets_dir, w, h, spp, frame=frame)
+    scenes = json.load(open(os.path.join(GOLDEN, "anim_scene_s4096_4k.json")))
+    assert (scenes["width"], scenes["height"], scenes["spp"]) == (w, h, spp)
+    assert scene_frame_hashes(s.view()) == scenes["frames"][str(frame)]
     arr = arrays_copy(s)
     gpu.upload_arrays(arr)
     bgra, acc = gpu.render(s.cfg, want_accum=True)
     gpu.synchronize()
-    rects = [(0, 0, 2, 2), (1900, 1000, 4, 4), (3000, 1500, 4, 2), (2400, 1200, 2, 4), (3836, 2158, 4, 2)]
+    ref = np.load(os.path.join(GOLDEN, "config4_spots.npz"))
+    assert (int(ref["width"]), int(ref["height"]), int(ref["spp"]), int(ref["frame"])) == (w, h, spp, frame)
+    rects = [tuple(int(v) for v in r) for r in ref["rects"]]
     acc_h = acc.cpu().numpy()
     bgra_h = bgra.cpu().numpy()
     orc = Oracle(arr, s.cfg)
+    k = 0
     for x0, y0, rw, rh in rects:
+        got_acc = _bits(acc_h[y0:y0 + rh, x0:x0 + rw, :3])
+        got_bgra = bgra_h[y0:y0 + rh, x0:x0 + rw]
+        n = rw * rh
+        assert np.array_equal(got_acc.reshape(-1, 3), ref["acc_bits"][k:k + n]), ("reference", x0, y0)
+        assert np.array_equal(got_bgra.reshape(-1, 4), ref["bgra"][k:k + n]), ("reference", x0, y0)
+        k += n
         acc_o, bgra_o = orc.render_rect(x0, y0, rw, rh)
-        assert np.array_equal(_bits(acc_h[y0:y0 + rh, x0:x0 + rw, :3]), _bits(acc_o[..., :3])), (x0, y0)
-        assert np.array_equal(bgra_h[y0:y0 + rh, x0:x0 + rw], bgra_o), (x0, y0)
+        assert np.array_equal(got_acc, _bits(acc_o[..., :3])), ("oracle", x0, y0)
+        assert np.array_equal(got_bgra, bgra_o), ("oracle", x0, y0)
     assert np.isfinite(acc_h).all() and (bgra_h[..., 3] == 255).all()

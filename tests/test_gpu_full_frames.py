@@ -1,0 +1,39 @@
+"""Whole frames at the bench's own workload against the reference itself
+(VERDICT r03 item 3): 1280x720 x 1024 spp, 4 bounces - BASELINE.json's metric
+configuration - frames 0 (the metric frame) and 450 (its heavy companion).
+
+The reference built from its own sources (strict IEEE build, oracle/Makefile)
+rendered both frames whole with baseline_render's semantics (main.cc:12-46:
+j-ordered float32 sum over 1024 samples, /SPP, tonemap_pixel) and hashed the
+averaged radiance bits and the BGRA bytes (tests/golden/make_anim_golden.py
+full1024 -> full_render_s1024.json; ~0.9 G samples per frame on the CPU).
+The product path (host setup_frame, ptg_upload_frame, ptg_render) must give
+both hashes exactly: every one of the 921,600 pixels bit-identical.  The
+frame's scene arrays (128 subframes) are checked against the reference's
+per-frame hashes first (anim_scene_s1024.json)."""
+import json
+import os
+
+import pytest
+
+from anim_check import image_hashes, scene_frame_hashes
+from conftest import GOLDEN, scene_for
+
+pytestmark = pytest.mark.gpu
+
+W, H, SPP = 1280, 720, 1024
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("frame", [0, 450])
+def test_whole_frame_bit_identical_to_reference(gpu, assets_dir, frame):
+    golden = json.load(open(os.path.join(GOLDEN, "full_render_s1024.json")))
+    assert (golden["width"], golden["height"], golden["spp"]) == (W, H, SPP)
+    scenes = json.load(open(os.path.join(GOLDEN, "anim_scene_s1024.json")))["frames"]
+    s = scene_for(assets_dir, W, H, SPP, frame=frame)
+    assert scene_frame_hashes(s.view()) == scenes[str(frame)]
+    gpu.upload(s, include_static=True)
+    bgra, acc = gpu.render(s.cfg, want_accum=True)
+    gpu.synchronize()
+    got = image_hashes(acc.cpu().numpy(), bgra.cpu().numpy())
+    assert got == golden["frames"][str(frame)], "frame %d differs from the reference's whole image" % frame

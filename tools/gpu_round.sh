@@ -36,7 +36,7 @@ for step in ${STEPS:-tests smoke}; do
                done ;;
     tests) run gpu_tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} || exit $? ;;
     debugtests) PTG_LIB=$P/ablate_debug/libptg.so run gpu_tests_ptg_debug 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --deselect tests/test_gpu_animation.py::test_every_frame_bit_identical_to_reference || exit $? ;;
-    profile) run profile_${PROF_TAG:-r03} 1000 bash tools/profile_gpu.sh ${PROF_TAG:-r03} || exit $? ;;
+    profile) run profile_${PROF_TAG:-r03} 1000 bash tools/profile_gpu.sh ${PROF_TAG:-r03} ${PROF_ARGS} || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     exf64) run exhaustive_f64 1100 tools/exhaustive_f64.sh; rc=$?; [ $rc -le 1 ] || exit $rc ;;
     exf64bin) for fn in ${FNS:-0 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17 18}; do

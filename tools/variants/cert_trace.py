@@ -15,9 +15,13 @@ __device__ inline void cert_record(double a, double b, double c, double d)
     if(k < 64) { g_cert_vals[4 * k] = a; g_cert_vals[4 * k + 1] = b; g_cert_vals[4 * k + 2] = c; g_cert_vals[4 * k + 3] = d; }
 }
 """ + a)
-b = "    mp.check(r >= 0.0f && (zero || (small && float_certain(v, margin))), v, CS_TIMES_ONE_MINUS_DIV_POW);"
-assert b in s
-s = s.replace(b, b + "\n    if(MP::kFast && !(r >= 0.0f && (zero || (small && float_certain(v, margin))))) cert_record(r, x, q, v);")
+# anchored on the site name: the statement `mp.check(<certain>, v, CS_TIMES_ONE_MINUS_DIV_POW);`
+# (possibly over several lines), whatever its condition currently reads
+import re
+m = re.search(r"mp\.check\(([^;]*?), v,\s*CS_TIMES_ONE_MINUS_DIV_POW\);", s)
+assert m, "certificate site CS_TIMES_ONE_MINUS_DIV_POW not found"
+cond = " ".join(m.group(1).split())
+s = s[:m.end()] + "\n    if(MP::kFast && !(%s)) cert_record(r, x, q, v);" % cond + s[m.end():]
 open(p, "w").write(s)
 p = sys.argv[1] + "/pt_kernels.hip"
 s = open(p).read()

@@ -16,6 +16,7 @@
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/block_bvh.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/hmath.h"
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -37,6 +38,7 @@ struct Res {
     float t = -1.0f, u = 0, v = 0;
     uint32_t inst = 0xFFFFFFFFu, prim = 0;
     bool back = false, occluded = false;
+    uint32_t occ_inst = 0xFFFFFFFFu, occ_prim = 0;   // any hit: the accepted triangle (not compared)
     bool operator==(const Res& r) const
     {
         return memcmp(&t, &r.t, 4) == 0 && memcmp(&u, &r.u, 4) == 0 && memcmp(&v, &r.v, 4) == 0 && inst == r.inst &&
@@ -174,6 +176,7 @@ Res link_walk(const ptg_scene_view& v, const Query& q, Stats& st)
 }
 
 constexpr uint32_t POP = 0xFFFFFFFFu;
+double g_last_split[3];   // block_walk: TLAS block steps, steps in the last BLAS, BLAS entries (OCC model)
 
 // ---- block walk (production packer, device algorithm) -----------------------
 bool g_spec = true;   // SPEC=0: no parked triangles
@@ -204,6 +207,8 @@ struct SimWalker {
     Blas b{};
     Res best;
     bool spec;
+    uint32_t skip = 0xFFFFFFFFu;   // OCC model: an instance not to enter (walked first already)
+    double tl_steps = 0, blas_cur = 0, enters_n = 0;   // OCC model: TLAS block steps, steps in the current BLAS, entries
 
     SimWalker(const ptg_scene_view& v_, const Packed& pk_, const Query& q_, Stats& st_, uint32_t C_, bool spec_)
         : v(v_), pk(pk_), q(q_), st(st_), C(C_), spec(spec_)
@@ -288,6 +293,8 @@ struct SimWalker {
     }
     int block_step()
     {
+        if(axis < 0) tl_steps++;
+        else blas_cur++;
         st.steps++;
         st.block_steps++;
         st.bytes += 128;
@@ -301,6 +308,44 @@ struct SimWalker {
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
+        // ORDER experiments (model only): 0 = the stored octant order (the
+        // reference's); 1 = nearest entry first; 2 = reversed; 3 = largest box
+        // first.  ANYORDER applies to any-hit queries, CLOSEORDER to closest-hit.
+        static const int any_order = getenv("ANYORDER") ? atoi(getenv("ANYORDER")) : 0;
+        static const int close_order = getenv("CLOSEORDER") ? atoi(getenv("CLOSEORDER")) : 0;
+        static const int order_level = getenv("ORDERLEVEL") ? atoi(getenv("ORDERLEVEL")) : 0;   // 0 both, 1 TLAS only, 2 BLAS only
+        int order = q.any ? any_order : close_order;
+        if((order_level == 1 && axis >= 0) || (order_level == 2 && axis < 0)) order = 0;
+        if(order)
+        {
+            struct E { uint32_t a; float n, key; };
+            E es[kBlockWidth];
+            int ne = 0;
+            for(uint32_t j = 0; j < kBlockWidth; ++j)
+            {
+                const BlockCopy::Near& x = bc.n[j];
+                const float* xf = &bc.f[3 * j];
+                if(x.a & kBeNone) continue;
+                float n;
+                st.visits++;
+                if(!box(org, inv, q.tmin, tmax, &x.x, xf, n)) continue;
+                float key = float(j);
+                if(order == 1) key = n;
+                else if(order == 2) key = -float(j);
+                else if(order == 3)
+                {
+                    const float dx = std::fabs(xf[0] - x.x), dy = std::fabs(xf[1] - x.y), dz = std::fabs(xf[2] - x.z);
+                    key = -(dx * dy + dy * dz + dz * dx);
+                }
+                es[ne++] = E{x.a, n, key};
+            }
+            std::stable_sort(es, es + ne, [](const E& a, const E& b) { return a.key < b.key; });
+            for(int k = ne - 1; k >= 1; --k) push(es[k].a, es[k].n);
+            cur = ne ? es[0].a : kBePop;
+            cnear = ne ? es[0].n : 0.0f;
+            park();
+            return 0;
+        }
         for(int j = int(kBlockWidth) - 1; j >= 0; --j)
         {
             const BlockCopy::Near& x = bc.n[j];
@@ -333,6 +378,7 @@ struct SimWalker {
     int tri_at(uint32_t id, float n)
     {
         if(!(n < tmax)) return 0;
+        blas_cur++;
         st.steps++;
         st.leaf_steps++;
         st.tri++;
@@ -341,7 +387,7 @@ struct SimWalker {
         Res c;
         if(tri(b, v, id, q.tmin, tmax, c))
         {
-            if(q.any) { best.occluded = true; return 2; }
+            if(q.any) { best.occluded = true; best.occ_inst = b.id; best.occ_prim = id; return 2; }
             best = c;
             tmax = c.t;
         }
@@ -363,6 +409,9 @@ struct SimWalker {
         cur = kBePop;
         if(axis < 0)
         {
+            if(id == skip) return 0;   // OCC model: this instance was walked first
+            enters_n++;
+            blas_cur = 0;
             st.steps++;
             st.leaf_steps++;
             st.enters++;
@@ -402,6 +451,9 @@ Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats&
         st.iters++;
     }
     st.depth_hist[w.maxd]++;
+    g_last_split[0] = w.tl_steps;
+    g_last_split[1] = w.blas_cur;
+    g_last_split[2] = w.enters_n;
     return w.best;
 }
 
@@ -558,6 +610,297 @@ int main(int argc, char** argv)
         printf("lockstep camera-ray waves: %.1f iterations, %.1f node phases with steps, %.1f%% on one block, %.1f blocks per phase\n",
                iters / 200, phases / 200, 100 * uniform / phases, distinct / phases);
         return 0;
+    }
+
+    if(getenv("OCC"))
+    {   // Any-hit occluder cache model.  trace_shadow_ray (path_tracer.hh:415-427)
+        // returns only whether ray_query_proceed found a candidate; with tmax
+        // fixed (no confirm) the result is the OR over triangles of "the TLAS
+        // leaf box, the BLAS leaf box and the triangle test all pass" (ancestors
+        // pass by containment).  So testing ANY candidate (instance, triangle)
+        // with exactly those three tests first is exact: an accept means
+        // "occluded".  This model measures how often cheap candidates exist and
+        // hit, and what the walks they replace cost.
+        //   wavefront query mix: waves of 8 pixels x 8 jittered samples (one
+        //   subframe), up to 4 bounces, a shadow ray toward the sun (within its
+        //   4-degree cone) from every hit lit from the viewer's side.
+        const uint32_t nwaves = paths / 64 ? paths / 64 : 1;
+        const double cos_cone = std::cos(4.0 * M_PI / 180.0);
+        // per subframe: instance -> its TLAS leaf box (the reference's node)
+        std::vector<std::map<uint32_t, std::pair<std::array<float, 3>, std::array<float, 3>>>> tleaf(v.subframe_count);
+        for(size_t sf = 0; sf < v.subframe_count; ++sf)
+        {
+            const ptg_bvh tl = v.subframes[sf].tlas;
+            const ptg_bvh_node* N = v.nodes + tl.node_offset;
+            const ptg_bvh_link* K = v.links + size_t(tl.node_offset) * 8;
+            for(uint32_t n = 0; n < tl.node_count; ++n)
+                if(K[n].accept & 0x80000000u)
+                    tleaf[sf][K[n].accept & 0x7FFFFFFFu] = {{N[n].min_x, N[n].min_y, N[n].min_z}, {N[n].max_x, N[n].max_y, N[n].max_z}};
+        }
+        uint64_t tests = 0, test_fail_membership = 0, wrong = 0;
+        auto cache_test = [&](const Query& q, uint32_t inst, uint32_t prim) -> bool {
+            ++tests;
+            auto it = tleaf[q.subframe].find(inst);
+            if(it == tleaf[q.subframe].end()) { ++test_fail_membership; return false; }
+            float nv;
+            const f3 winv = v3(srcp(q.d.x), srcp(q.d.y), srcp(q.d.z));
+            if(!box(q.o, winv, q.tmin, q.tmax, it->second.first.data(), it->second.second.data(), nv)) return false;
+            const ptg_tlas_instance& in = v.instances[inst];
+            if(prim >= in.m.triangle_count) return false;
+            const Blas b = enter(in, inst, q.o, q.d);
+            const uint32_t* t = v.indices + in.m.index_offset + size_t(prim) * 3;
+            const ptg_float3* P = v.pos + in.m.base_vertex_offset;
+            const ptg_float3 &A = P[t[0]], &B = P[t[1]], &C = P[t[2]];
+            // the BLAS leaf's box: fmin / fmax of the triangle's vertices (bvh.cc:243-246)
+            const float lo[3] = {fminf_(A.x, fminf_(B.x, C.x)), fminf_(A.y, fminf_(B.y, C.y)), fminf_(A.z, fminf_(B.z, C.z))};
+            const float hi[3] = {fmaxf_(A.x, fmaxf_(B.x, C.x)), fmaxf_(A.y, fmaxf_(B.y, C.y)), fmaxf_(A.z, fmaxf_(B.z, C.z))};
+            if(!box(b.org, b.inv, q.tmin, q.tmax, lo, hi, nv)) return false;
+            Res c;
+            return tri(b, v, prim, q.tmin, q.tmax, c);
+        };
+        // instance-first walk: the TLAS leaf box of `inst`, then its BLAS walked
+        // whole (any hit) before the TLAS; on no hit the normal walk follows,
+        // skipping `inst` (walking it again cannot accept).  Returns the steps
+        // of both parts; `occ` = the result (must equal the reference's).
+        auto inst_first = [&](const Query& q, uint32_t inst, bool& occ, uint32_t prim = 0xFFFFFFFFu) -> double {
+            Stats st;
+            occ = false;
+            if(prim != 0xFFFFFFFFu && cache_test(q, inst, prim)) { occ = true; return 2.0; }   // the triangle first
+            if(prim != 0xFFFFFFFFu) st.steps += 1;
+            auto it = tleaf[q.subframe].find(inst);
+            float nv;
+            const f3 winv = v3(srcp(q.d.x), srcp(q.d.y), srcp(q.d.z));
+            bool entered = false;
+            if(it != tleaf[q.subframe].end() &&
+               box(q.o, winv, q.tmin, q.tmax, it->second.first.data(), it->second.second.data(), nv))
+            {
+                entered = true;
+                SimWalker w(v, pk, q, st, S, g_spec);
+                w.cur = kBeLeaf | inst;
+                w.cnear = nv;
+                for(;;)
+                {
+                    int r = 0;
+                    for(int u = 0; u < 2 && r == 0; ++u)
+                        if(!w.at_leaf()) r = w.node_step();
+                    if(r == 0 && w.wants_leaf()) r = w.leaf_step();
+                    if(r) { occ = r == 2; break; }
+                }
+            }
+            if(occ) return st.steps + 1;
+            SimWalker w(v, pk, q, st, S, g_spec);
+            if(entered) w.skip = inst;
+            for(;;)
+            {
+                int r = 0;
+                for(int u = 0; u < 2 && r == 0; ++u)
+                    if(!w.at_leaf()) r = w.node_step();
+                if(r == 0 && w.wants_leaf()) r = w.leaf_step();
+                if(r) { occ = r == 2; break; }
+            }
+            return st.steps + 1;
+        };
+        struct SQ { Query q; bool occ; uint32_t oi, op; double steps, block; uint32_t pixel; double tl, last, enters; };
+        // shadow queries by [round][wave][lane] (absent: subframe == ~0u)
+        std::vector<std::vector<SQ>> sq(4, std::vector<SQ>(size_t(nwaves) * 64));
+        for(auto& r: sq) for(auto& x: r) x.q.subframe = ~0u;
+        const uint32_t row0 = uint32_t(rnd() * (cfg.height - nwaves / 160 - 1));
+        for(uint32_t w = 0; w < nwaves; ++w)
+        {
+            const uint32_t sf = uint32_t(rnd() * v.subframe_count) % v.subframe_count;
+            const ptg_camera& cam = v.subframes[sf].cam;
+            const f3 L0 = normalize(v.subframes[sf].light.direction);
+            for(uint32_t l = 0; l < 64; ++l)
+            {
+                const uint32_t px = (8 * w + l / 8) % cfg.width, py = row0 + (8 * w + l / 8) / cfg.width;
+                float ux = (px + rnd()) / cfg.width * 2.0f - 1.0f, uy = (py + rnd()) / cfg.height * 2.0f - 1.0f;
+                ux *= cam.aspect_ratio;
+                uy = -uy;
+                f3 d = normalize(mul_m3v3(cam.orientation, normalize(v3(ux * cam.inv_focal_length, uy * cam.inv_focal_length, -1.0f))));
+                f3 o = cam.position;
+                for(uint32_t bnc = 0; bnc < 4; ++bnc)
+                {
+                    Stats tmp;
+                    const Res r = link_walk(v, Query{o, d, bnc ? 1e-4f : 0.0f, 1e9f, sf, false}, tmp);
+                    if(r.inst == 0xFFFFFFFFu) break;
+                    const ptg_tlas_instance& in = v.instances[r.inst];
+                    const uint32_t* t = v.indices + in.m.index_offset + size_t(r.prim) * 3;
+                    const ptg_float3* P = v.pos + in.m.base_vertex_offset;
+                    const f3 A = v3(P[t[0]].x, P[t[0]].y, P[t[0]].z), B = v3(P[t[1]].x, P[t[1]].y, P[t[1]].z),
+                             C = v3(P[t[2]].x, P[t[2]].y, P[t[2]].z);
+                    const f3 ng = normalize(mul_m3v3(extract(in.transform), cross(B - A, C - A)));
+                    o = o + d * r.t;
+                    // a direction in the sun's cone
+                    f3 L;
+                    {
+                        const double z = 1.0 - rnd() * (1.0 - cos_cone), ph = 2 * M_PI * rnd(), rr = std::sqrt(std::max(0.0, 1 - z * z));
+                        const f3 up = std::fabs(L0.x) < 0.9f ? v3(1, 0, 0) : v3(0, 1, 0);
+                        const f3 T = normalize(cross(up, L0)), Bt = cross(L0, T);
+                        L = normalize(T * float(rr * std::cos(ph)) + Bt * float(rr * std::sin(ph)) + L0 * float(z));
+                    }
+                    if(dot(ng, L) * dot(ng, -d) > 0)   // lit from the viewer's side: the NEE ray is traced
+                    {
+                        SQ& x = sq[bnc][size_t(w) * 64 + l];
+                        x.q = Query{o, L, 1e-4f, 1e9f, sf, true, bnc, r.inst};
+                        x.pixel = py * cfg.width + px;
+                        Stats st;
+                        const Res br = block_walk(v, pk, x.q, st, S);
+                        Stats lt;
+                        if(!(link_walk(v, x.q, lt) == br)) ++wrong;
+                        x.occ = br.occluded;
+                        x.oi = br.occ_inst;
+                        x.op = br.occ_prim;
+                        x.steps = st.steps;
+                        x.block = st.block_steps;
+                        x.tl = g_last_split[0];
+                        x.last = g_last_split[1];
+                        x.enters = g_last_split[2];
+                    }
+                    // next bounce: a random direction on the viewer's side of the surface
+                    f3 nd;
+                    do { nd = v3(rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1); } while(dot(nd, nd) > 1 || dot(nd, nd) < 1e-4f);
+                    nd = normalize(nd);
+                    if(dot(nd, ng) * dot(-d, ng) < 0) nd = -nd;
+                    d = nd;
+                }
+            }
+        }
+        // policies: P = the path's previous occluder; W = occluders found by the wave's
+        // earlier lanes this round (most recent K); X = the pixel's last occluder at this
+        // round (earlier sample groups); N = the previous wave's occluders this round
+        const int K = getenv("OCCK") ? atoi(getenv("OCCK")) : 2;
+        const char* names[] = {"P (path)", "W (wave, last K)", "X (pixel)", "N (prev wave)", "P+W", "P+W+X"};
+        const int NP = 6;
+        double tot_q = 0, tot_occ = 0, steps_all = 0, steps_occ = 0, block_all = 0;
+        double have[NP] = {}, hit[NP] = {}, saved[NP] = {}, ntest[NP] = {};
+        for(int r = 0; r < 4; ++r)
+        {
+            std::map<uint32_t, std::pair<uint32_t, uint32_t>> pix;
+            std::vector<std::pair<uint32_t, uint32_t>> prevwave;
+            for(uint32_t w = 0; w < nwaves; ++w)
+            {
+                std::vector<std::pair<uint32_t, uint32_t>> wave;   // this round's occluders, lane order
+                for(uint32_t l = 0; l < 64; ++l)
+                {
+                    const SQ& x = sq[r][size_t(w) * 64 + l];
+                    if(x.q.subframe == ~0u) continue;
+                    tot_q++;
+                    steps_all += x.steps;
+                    block_all += x.block;
+                    if(x.occ) { tot_occ++; steps_occ += x.steps; }
+                    std::vector<std::pair<uint32_t, uint32_t>> cands[NP];
+                    for(int pr = r - 1; pr >= 0; --pr)
+                    {
+                        const SQ& y = sq[pr][size_t(w) * 64 + l];
+                        if(y.q.subframe != ~0u && y.occ) { cands[0].push_back({y.oi, y.op}); break; }
+                    }
+                    for(int k = int(wave.size()) - 1; k >= 0 && int(wave.size()) - k <= K; --k) cands[1].push_back(wave[k]);
+                    if(auto it = pix.find(x.pixel); it != pix.end()) cands[2].push_back(it->second);
+                    for(int k = int(prevwave.size()) - 1; k >= 0 && int(prevwave.size()) - k <= K; --k) cands[3].push_back(prevwave[k]);
+                    cands[4] = cands[0];
+                    cands[4].insert(cands[4].end(), cands[1].begin(), cands[1].end());
+                    cands[5] = cands[4];
+                    cands[5].insert(cands[5].end(), cands[2].begin(), cands[2].end());
+                    for(int pi = 0; pi < NP; ++pi)
+                    {
+                        // distinct candidates in order
+                        std::vector<std::pair<uint32_t, uint32_t>> c;
+                        for(auto& e: cands[pi]) if(std::find(c.begin(), c.end(), e) == c.end()) c.push_back(e);
+                        if(c.empty()) continue;
+                        have[pi]++;
+                        bool ok = false;
+                        for(auto& e: c)
+                        {
+                            ntest[pi]++;
+                            if(cache_test(x.q, e.first, e.second)) { ok = true; break; }
+                        }
+                        if(ok)
+                        {
+                            if(!x.occ) ++wrong;   // an accepted candidate must mean "occluded"
+                            hit[pi]++;
+                            saved[pi] += x.steps;
+                        }
+                    }
+                    if(x.occ)
+                    {
+                        wave.push_back({x.oi, x.op});
+                        pix[x.pixel] = {x.oi, x.op};
+                    }
+                }
+                prevwave = wave;
+            }
+        }
+        {
+            double a[2][5] = {};
+            for(auto& rr: sq)
+                for(auto& x: rr)
+                    if(x.q.subframe != ~0u)
+                    {
+                        double* t = a[x.occ ? 1 : 0];
+                        t[0]++; t[1] += x.steps; t[2] += x.tl; t[3] += x.last; t[4] += x.enters;
+                    }
+            for(int k = 0; k < 2; ++k)
+                printf("%s queries: %.0f, steps %.2f = TLAS blocks %.2f + BLAS entries %.2f + steps in BLASes %.2f, of which "
+                       "the last BLAS %.2f\n", k ? "occluded" : "unoccluded", a[k][0], a[k][1] / a[k][0], a[k][2] / a[k][0],
+                       a[k][4] / a[k][0], (a[k][1] - a[k][2] - a[k][4]) / a[k][0], a[k][3] / a[k][0]);
+        }
+        printf("occluder model, frame %u: %.0f shadow queries (%.1f per path), %.1f%% occluded; block-walk steps per query %.2f "
+               "(block %.2f); occluded queries carry %.1f%% of the steps\n",
+               frame, tot_q, tot_q / (nwaves * 64.0), 100 * tot_occ / tot_q, steps_all / tot_q, block_all / tot_q,
+               100 * steps_occ / steps_all);
+        for(int pi = 0; pi < NP; ++pi)
+            printf("  %-18s candidate for %5.1f%% of queries, hits %5.1f%% of occluded queries, %.2f tests per query with one; "
+                   "steps saved %5.1f%% (net of 1 step per test: %5.1f%%)\n",
+                   names[pi], 100 * have[pi] / tot_q, 100 * hit[pi] / std::max(1.0, tot_occ), ntest[pi] / std::max(1.0, have[pi]),
+                   100 * saved[pi] / steps_all, 100 * (saved[pi] - ntest[pi]) / steps_all);
+        // instance level: the candidate instance's BLAS walked first
+        {
+            const char* in_names[] = {"Pi (path)", "Wi (wave, last)", "Xi (pixel)", "Pi else Wi", "Pi else Xi else Wi",
+                                      "(P else W) tri+inst", "(W) tri+inst"};
+            const int NI = 7;
+            double cost[NI] = {}, have_i[NI] = {}, hit_i[NI] = {};
+            for(int r = 0; r < 4; ++r)
+            {
+                std::map<uint32_t, uint32_t> pix;
+                for(uint32_t w = 0; w < nwaves; ++w)
+                {
+                    uint32_t wave_last = 0xFFFFFFFFu, wave_last_p = 0xFFFFFFFFu;
+                    for(uint32_t l = 0; l < 64; ++l)
+                    {
+                        const SQ& x = sq[r][size_t(w) * 64 + l];
+                        if(x.q.subframe == ~0u) continue;
+                        uint32_t pc = 0xFFFFFFFFu, pp = 0xFFFFFFFFu, xc = 0xFFFFFFFFu;
+                        for(int pr = r - 1; pr >= 0; --pr)
+                        {
+                            const SQ& y = sq[pr][size_t(w) * 64 + l];
+                            if(y.q.subframe != ~0u && y.occ) { pc = y.oi; pp = y.op; break; }
+                        }
+                        if(auto it = pix.find(x.pixel); it != pix.end()) xc = it->second;
+                        const uint32_t cand[NI] = {pc, wave_last, xc, pc != ~0u ? pc : wave_last,
+                                                   pc != ~0u ? pc : (xc != ~0u ? xc : wave_last),
+                                                   pc != ~0u ? pc : wave_last, wave_last};
+                        const uint32_t cprim[NI] = {~0u, ~0u, ~0u, ~0u, ~0u, pc != ~0u ? pp : wave_last_p, wave_last_p};
+                        for(int pi = 0; pi < NI; ++pi)
+                        {
+                            if(cand[pi] == ~0u) { cost[pi] += x.steps; continue; }
+                            have_i[pi]++;
+                            bool occ;
+                            cost[pi] += inst_first(x.q, cand[pi], occ, cprim[pi]);
+                            if(occ != x.occ) ++wrong;
+                            hit_i[pi] += (occ && x.occ) ? 1 : 0;
+                        }
+                        if(x.occ) { wave_last = x.oi; wave_last_p = x.op; pix[x.pixel] = x.oi; }
+                    }
+                }
+            }
+            for(int pi = 0; pi < NI; ++pi)
+                printf("  instance-first %-20s candidate for %5.1f%%, occluded via it or after %5.1f%% of occluded; steps %+.1f%% vs the walk\n",
+                       in_names[pi], 100 * have_i[pi] / tot_q, 100 * hit_i[pi] / std::max(1.0, tot_occ), 100 * (cost[pi] - steps_all) / steps_all);
+        }
+        printf("  %llu wrong (block walk vs link walk, or an accepted candidate on an unoccluded ray); %llu of %llu tests "
+               "failed the TLAS membership\n", (unsigned long long)wrong, (unsigned long long)test_fail_membership,
+               (unsigned long long)tests);
+        return wrong ? 1 : 0;
     }
 
     // the query mix
