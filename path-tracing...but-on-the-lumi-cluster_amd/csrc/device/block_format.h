@@ -51,7 +51,7 @@
 //     rows 4-6   the four entries' far.xyz, packed (f[3j .. 3j+2])
 //     a: kBeLeaf | payload   leaf (BLAS: triangle index in the mesh,
 //                            TLAS: instance index), payload < 2^28
-//        kBeNone             unused slot (NaN box, never passes)
+//        kBeNone             unused slot (planes at +-inf: near +inf, far -inf for the copy's octant; never passes)
 //        otherwise           block index of the child's own block
 //   octant o's copy of block k: blocks[k * 8 + o]
 // A BVH's handle is its root block's index; the root's own box is never

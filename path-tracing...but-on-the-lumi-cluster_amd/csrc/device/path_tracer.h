@@ -424,15 +424,29 @@ struct BlockWalker {
     // then t of the near plane IS fmin(t0, t1) of the reference's per-axis
     // pair (the product of the ordered differences with a finite nonzero
     // reciprocal keeps their order; equal values are equal), so the per-axis
-    // min/max drop out.  An unused slot's NaN planes fail it like any miss.
-    PTG_D bool box_near_far(float4 nr, float4 fr, float& nearv) const
+    // min/max drop out.
+    //
+    // The three compares become one by clamping the interval: with tmin >= 0,
+    // tmax > 0 finite, tmin_p the float after tmin and tmax_m the one before
+    // tmax (integer +-1 on the bits; f32 denormals are kept, so the compares
+    // see them exactly),
+    //   near <= far && far > tmin && near < tmax
+    //     <=>  max(near, tmin_p) <= min(far, tmax_m)   whenever tmin_p <= tmax_m,
+    // and the returned entry distance max(near, tmin_p) re-checks at its pop
+    // as near does: max(near, tmin_p) < tmax <=> near < tmax whenever
+    // tmin_p < tmax.  When tmax <= tmin_p no float t has tmin < t < tmax, so
+    // no triangle can be accepted any more and which boxes pass changes
+    // nothing.  No NaN arises (finite planes, finite reciprocals); an unused
+    // slot's planes are +-inf so that its near is +inf and its far -inf
+    // (host/block_bvh.cpp), which fails.
+    PTG_D bool box_near_far(float4 nr, float4 fr, float tmin_p, float tmax_m, float& nearv) const
     {
         const float tnx = (nr.x - org.x) * inv.x, tfx = (fr.x - org.x) * inv.x;
         const float tny = (nr.y - org.y) * inv.y, tfy = (fr.y - org.y) * inv.y;
         const float tnz = (nr.z - org.z) * inv.z, tfz = (fr.z - org.z) * inv.z;
-        nearv = fmaxf(tnx, fmaxf(tny, tnz));
-        const float farv = fminf(tfx, fminf(tfy, tfz));
-        return nearv <= farv && farv > tmin && nearv < tmax;
+        nearv = fmaxf(fmaxf(tnx, tmin_p), fmaxf(tny, tnz));
+        const float farv = fminf(fminf(tfx, tmax_m), fminf(tfy, tfz));
+        return nearv <= farv;
     }
 
     // ray_query_enter_blas (ray_query.hh:153-182) with instance `leaf`'s record:
@@ -575,7 +589,6 @@ struct BlockWalker {
         float4 l[W], h[W];
         uint32_t a[W];
         float nr[W];
-        bool pass[W];
 #pragma unroll
         for(uint32_t j = 0; j < W; ++j)
         {
@@ -584,16 +597,23 @@ struct BlockWalker {
             a[j] = __float_as_uint(l[j].w);
         }
         if(COUNT) cnt.step_loads |= 1u;
+        // bit j: the entry the ray meets j-th passed.  Built inside each form's
+        // branch, so the two branches merge an integer, not four lane masks
+        // (a merge of lane masks costs exec-masked scalar and/or per mask)
+        uint32_t hits = 0;
         if(__all(fin))
         {   // every lane's reciprocal finite (the rule): no per-axis min/max
+            const float tmin_p = __uint_as_float(__float_as_uint(tmin) + 1u);
+            const float tmax_m = __uint_as_float(__float_as_uint(tmax) - 1u);
 #pragma unroll
-            for(uint32_t j = 0; j < W; ++j) pass[j] = box_near_far(l[j], h[j], nr[j]);
+            for(uint32_t j = 0; j < W; ++j) hits |= box_near_far(l[j], h[j], tmin_p, tmax_m, nr[j]) ? (1u << j) : 0u;
         }
         else
         {   // a lane with a zero or denormal direction component: the
-            // reference's min/max form (an unordered pair gives the same)
+            // reference's min/max form (an unordered pair gives the same);
+            // an infinite reciprocal can pass an unused slot's infinite planes
 #pragma unroll
-            for(uint32_t j = 0; j < W; ++j) pass[j] = box(l[j], h[j], nr[j]);
+            for(uint32_t j = 0; j < W; ++j) hits |= (box(l[j], h[j], nr[j]) && !(a[j] & kBeNone)) ? (1u << j) : 0u;
         }
         if(COUNT)
         {
@@ -603,11 +623,8 @@ struct BlockWalker {
             cnt.visits += tested;
             if(axis < 0) cnt.tlas_visits += tested;
         }
-        // bit j: the entry the ray meets j-th passed.  The first is walked
-        // next; the others are pushed last-first, so they pop in order.
-        uint32_t hits = 0;
-#pragma unroll
-        for(uint32_t j = 0; j < W; ++j) hits |= pass[j] ? (1u << j) : 0u;
+        // The first entry that passed is walked next; the others are pushed
+        // last-first, so they pop in order.
         const uint32_t first = uint32_t(__builtin_ctz(hits | (1u << W))) & (W - 1u);
         uint32_t fa, fn;   // entry `first`, by value (v_cndmask): neither a branch nor an indexed copy
         if constexpr(W == 4)

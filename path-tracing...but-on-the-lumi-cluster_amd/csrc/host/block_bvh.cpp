@@ -235,10 +235,17 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
             for(uint32_t j = 0; j < W; ++j)
             {
                 if(j >= seq.size())
-                {   // an unused slot: a NaN box never passes
-                    const float q = std::numeric_limits<float>::quiet_NaN();
-                    bc.n[j] = BlockCopy::Near{q, q, q, kBeNone};
-                    bc.f[3 * j] = bc.f[3 * j + 1] = bc.f[3 * j + 2] = q;
+                {   // an unused slot: planes at +-inf such that, for a ray of this
+                    // octant (its reciprocal's sign per axis is the octant's), the
+                    // near plane's t is +inf and the far plane's -inf - it never
+                    // passes the walker's clamped test (BlockWalker::box_near_far);
+                    // the min/max form checks kBeNone
+                    const float inf = std::numeric_limits<float>::infinity();
+                    const bool px = o & 1u, py = o & 2u, pz = o & 4u;
+                    bc.n[j] = BlockCopy::Near{px ? inf : -inf, py ? inf : -inf, pz ? inf : -inf, kBeNone};
+                    bc.f[3 * j] = px ? -inf : inf;
+                    bc.f[3 * j + 1] = py ? -inf : inf;
+                    bc.f[3 * j + 2] = pz ? -inf : inf;
                     continue;
                 }
                 const uint32_t c = seq[j];

@@ -49,28 +49,21 @@ def levels_of(ent, ceil):
     return lv
 
 
-def main():
-    if len(sys.argv) > 1:
-        path = sys.argv[1]
-    else:   # the newest bench line whose roofline cites a committed PMC profile (config runs without one are skipped)
-        path = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line.json")), key=natural)
-                if "traffic_source" in (json.load(open(p)).get("roofline") or {})][-1]
-    line = json.load(open(path))
-    rf = line["roofline"]
-    prof_path = os.path.join(ROOT, rf["traffic_source"].split(" ")[0])
-    prof = json.load(open(prof_path))
-    ent = prof["extend"]
-    ceil = json.load(open(os.path.join(ROOT, rf["ceilings_source"])))
+TRACE_NAME = {"extend": "k_wf_walk<false, false>", "shadow": "k_wf_walk<true, false>"}
+
+
+def trace_ms_of(prof_path, kind):
     stats = os.path.join(os.path.dirname(prof_path), "kernel_stats.csv")
-    trace_ms = None
     for r in csv.DictReader(open(stats)):
-        if "k_wf_walk<false, false>" in r["Name"]:
-            trace_ms = float(r["AverageNs"]) / 1e6
-    iso_ms = rf["isolated"]["ms_per_launch"]
-    print("bench line:", os.path.relpath(path, ROOT))
-    print("PMC profile:", os.path.relpath(prof_path, ROOT), " ceilings:", rf["ceilings_source"])
-    print("launch time: isolated (HIP events) %.4f ms, rocprof trace avg %.4f ms" % (iso_ms, trace_ms))
-    ok = abs(trace_ms - iso_ms) <= 0.15 * iso_ms
+        if TRACE_NAME[kind] in r["Name"]:
+            return float(r["AverageNs"]) / 1e6
+    return None
+
+
+def check_levels(ent, ceil, iso_ms, trace_ms, want_levels, label):
+    """Recompute every level's floor; compare frac_isolated (and, where the line
+    has them, the count and ceiling) with the line.  Returns (ok, floors)."""
+    ok = True
     floors = {}
     print("%-11s %16s %16s %12s %10s %10s" % ("level", "count/launch", "ceiling/s", "floor ms", "frac_iso", "frac_rocprof"))
     for name, (count, rate) in levels_of(ent, ceil).items():
@@ -78,15 +71,65 @@ def main():
         floors[name] = t
         fi, fr = t / (iso_ms / 1e3), t / (trace_ms / 1e3)
         print("%-11s %16.4g %16.4g %12.4f %10.4f %10.4f" % (name, count, rate, t * 1e3, fi, fr))
-        want = rf["levels"][name]
+        want = want_levels[name]
         for k, mine in (("count_per_launch", count), ("ceiling_per_s", rate), ("frac_isolated", fi)):
+            if k not in want:
+                continue
             if abs(want[k] - mine) > 1e-3 * max(abs(want[k]), 1e-12) + 5e-4 * (k == "frac_isolated"):
-                print("  MISMATCH %s.%s: bench %r, recomputed %r" % (name, k, want[k], mine))
+                print("  MISMATCH %s %s.%s: bench %r, recomputed %r" % (label, name, k, want[k], mine))
                 ok = False
-    bound = max(floors, key=floors.get)
-    print("bound: %s (bench: %s); frac isolated %.4f (bench %.4f), frac rocprof %.4f" %
-          (bound, rf["bound"], floors[bound] / (iso_ms / 1e3), rf["isolated"]["frac"], floors[bound] / (trace_ms / 1e3)))
-    ok = ok and bound == rf["bound"] and abs(floors[bound] / (iso_ms / 1e3) - rf["isolated"]["frac"]) < 1e-3
+    return ok, floors
+
+
+def repro_roofline(rf, label):
+    """One roofline block of a bench line (the metric frame's or the heavy
+    frame's): the closest-hit walk's levels, then each walk's in `walks`."""
+    ok = True
+    if rf.get("traffic_source"):
+        prof_path = os.path.join(ROOT, rf["traffic_source"].split(" ")[0])
+        prof = json.load(open(prof_path))
+        ceil = json.load(open(os.path.join(ROOT, rf["ceilings_source"])))
+        trace_ms = trace_ms_of(prof_path, "extend")
+        iso_ms = rf["isolated"]["ms_per_launch"]
+        print("== %s: %s, PMC profile %s (workload %r), ceilings %s" % (label, rf.get("kernel"), os.path.relpath(prof_path, ROOT),
+                                                                     prof.get("_workload"), rf["ceilings_source"]))
+        print("launch time: isolated (HIP events) %.4f ms, rocprof trace avg %.4f ms" % (iso_ms, trace_ms))
+        ok = abs(trace_ms - iso_ms) <= 0.15 * iso_ms
+        lok, floors = check_levels(prof["extend"], ceil, iso_ms, trace_ms, rf["levels"], label)
+        bound = max(floors, key=floors.get)
+        print("bound: %s (bench: %s); frac isolated %.4f (bench %.4f), frac rocprof %.4f" %
+              (bound, rf["bound"], floors[bound] / (iso_ms / 1e3), rf["isolated"]["frac"], floors[bound] / (trace_ms / 1e3)))
+        ok = ok and lok and bound == rf["bound"] and abs(floors[bound] / (iso_ms / 1e3) - rf["isolated"]["frac"]) < 1e-3
+    for kind, wl in (rf.get("walks") or {}).items():
+        if not wl.get("source"):
+            continue
+        prof_path = os.path.join(ROOT, wl["source"])
+        prof = json.load(open(prof_path))
+        ceil = json.load(open(os.path.join(ROOT, rf.get("ceilings_source") or "profiles/r02_probe/ceilings.json")))
+        trace_ms = trace_ms_of(prof_path, kind)
+        iso_ms = wl["ms_per_launch_isolated"]
+        print("== %s, walk %s: isolated %.4f ms, rocprof trace avg %.4f ms" % (label, kind, iso_ms, trace_ms))
+        kok = abs(trace_ms - iso_ms) <= 0.15 * iso_ms
+        lok, floors = check_levels(prof[kind], ceil, iso_ms, trace_ms, wl["levels"], "%s/%s" % (label, kind))
+        bound = max(floors, key=floors.get)
+        print("bound: %s (bench: %s); frac isolated %.4f (bench %.4f)" %
+              (bound, wl["bound"], floors[bound] / (iso_ms / 1e3), wl["frac_isolated"]))
+        ok = ok and kok and lok and bound == wl["bound"] and abs(floors[bound] / (iso_ms / 1e3) - wl["frac_isolated"]) < 1e-3
+    return ok
+
+
+def main():
+    if len(sys.argv) > 1:
+        path = sys.argv[1]
+    else:   # the newest bench line whose roofline cites a committed PMC profile (config runs without one are skipped)
+        path = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line.json")), key=natural)
+                if "traffic_source" in (json.load(open(p)).get("roofline") or {})][-1]
+    line = json.load(open(path))
+    print("bench line:", os.path.relpath(path, ROOT))
+    ok = repro_roofline(line["roofline"], "metric frame")
+    heavy = (line.get("heavy_frame") or {}).get("roofline")
+    if heavy:
+        ok = repro_roofline(heavy, "heavy frame %d" % line["heavy_frame"]["frame"]) and ok
     print("reproduced" if ok else "NOT reproduced")
     return 0 if ok else 1
 

@@ -355,13 +355,18 @@ struct SimWalker {
             st.visits++;
             bool pass;
             if(fin)
-            {   // the device's fast form: near = max of near-plane t, far = min of far-plane t
+            {   // the device's fast form: near = max of near-plane t, far = min of far-plane t,
+                // the interval clamped to [next(tmin), prev(tmax)] (BlockWalker::box_near_far)
+                float tmin_p = q.tmin, tmax_m = tmax;
+                uint32_t bits;
+                memcpy(&bits, &tmin_p, 4); bits += 1; memcpy(&tmin_p, &bits, 4);
+                memcpy(&bits, &tmax_m, 4); bits -= 1; memcpy(&tmax_m, &bits, 4);
                 const float tnx = (x.x - org.x) * inv.x, tfx = (xf[0] - org.x) * inv.x;
                 const float tny = (x.y - org.y) * inv.y, tfy = (xf[1] - org.y) * inv.y;
                 const float tnz = (x.z - org.z) * inv.z, tfz = (xf[2] - org.z) * inv.z;
-                n = fmaxf_(tnx, fmaxf_(tny, tnz));
-                const float f = fminf_(tfx, fminf_(tfy, tfz));
-                pass = n <= f && f > q.tmin && n < tmax;
+                n = fmaxf_(fmaxf_(tnx, tmin_p), fmaxf_(tny, tnz));
+                const float f = fminf_(fminf_(tfx, tmax_m), fminf_(tfy, tfz));
+                pass = n <= f;
             }
             else
                 pass = box(org, inv, q.tmin, tmax, &x.x, xf, n);
