@@ -34,7 +34,10 @@ Multi-GPU: one process per GPU (torch.distributed.run).  --shard frames
 (default): rank r renders frame (frame + r) - weak scaling, no collective on
 the data path (BASELINE config 4 style).  --shard tiles: one frame split into
 interleaved 32x16 tiles, rank 0 gathers the BGRA tiles over RCCL and
-assembles the framebuffer - strong scaling (config 3 style).
+assembles the framebuffer - strong scaling (config 3 style).  --shard samples:
+one frame's samples split into whole motion-blur groups, rank 0 sum-reduces
+the radiance over RCCL and tonemaps it - strong scaling, within float32
+rounding of the single-GPU frame.
 """
 import argparse
 import json
@@ -337,7 +340,10 @@ def main():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--bounces", type=int, default=4)
-    ap.add_argument("--shard", choices=["frames", "tiles"], default="frames")
+    ap.add_argument("--shard", choices=["frames", "tiles", "samples"], default="frames",
+                    help="frames: rank r renders frame + r (weak scaling); tiles: one frame in interleaved tiles, "
+                         "one RCCL gather (strong, bit-identical); samples: one frame's sample range in whole "
+                         "motion-blur groups, one RCCL sum-reduce (strong, within float32 rounding)")
     ap.add_argument("--tile", type=str, default="32x16")
     ap.add_argument("--concurrency", type=int, default=2, choices=[0, 1, 2],
                     help="ptg_set_concurrency level of the timed steps (profiling passes use 0)")
@@ -431,9 +437,12 @@ def main():
     image = torch.empty((cfg.height, cfg.width, 4), dtype=torch.uint8, device=dev)
     accum = torch.empty((cfg.height, cfg.width, 4), dtype=torch.float32, device=dev)
     shard = D.TileShard(cfg, tw, th, rank, world) if args.shard == "tiles" else None
+    sshard = D.SampleShard(cfg, rank, world) if args.shard == "samples" else None
 
     def render_step():
-        if shard is None:
+        if sshard is not None:
+            D.render_and_reduce(r, cfg, sshard, image, accum=accum, stream=stream)
+        elif shard is None:
             r.render(cfg, out_bgra=image, out_accum=accum)   # the radiance too: the last step is hashed
         else:
             D.render_and_gather(r, cfg, shard, image, stream=stream)
@@ -491,8 +500,8 @@ def main():
     def frame_check(f):
         """This rank's last rendered frame (accum + image) against the reference's
         whole-image hashes of frame f at this configuration, if the golden holds it."""
-        if shard is not None:
-            return None
+        if shard is not None or (sshard is not None and (world > 1 or rank != 0)):
+            return None   # tiles: BGRA only; sample shards over N > 1 ranks sum in another order
         want = frame_golden(cfg, f)
         if want is None:
             return None
@@ -531,10 +540,10 @@ def main():
         if long_steps:
             print("counting pass", file=sys.stderr, flush=True)
         r.enable_counters(True)
-        if shard is None:
-            r.render(cfg, out_bgra=image)
-        else:
+        if shard is not None:
             r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+        else:
+            r.render(cfg, out_bgra=image, samples=(sshard.j0, sshard.j1) if sshard else None)
         r.synchronize()
         kc = r.kernel_counters()
         ws = r.walk_stats()
@@ -551,10 +560,10 @@ def main():
             print("isolated-walk pass", file=sys.stderr, flush=True)
         r.set_concurrency(0)
         r.enable_timing(True)
-        if shard is None:
-            r.render(cfg, out_bgra=image)
-        else:
+        if shard is not None:
             r.render_tiles(cfg, tw, th, shard.first, shard.stride, shard.count)
+        else:
+            r.render(cfg, out_bgra=image, samples=(sshard.j0, sshard.j1) if sshard else None)
         r.synchronize()
         kb_iso = r.kernel_busy()
         r.enable_timing(False)

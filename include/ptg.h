@@ -225,6 +225,9 @@ int ptg_path_trace_samples(ptg_context* ctx, const ptg_render_config* cfg, size_
 
 /* tonemap_pixel (path_tracer.hh:753) on n colours. HOST pointers; synchronous. */
 int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4* out);
+/* The same on DEVICE pointers, asynchronous on the context's stream (the
+ * sample-range shard tonemaps the reduced radiance with it). */
+int ptg_tonemap_device(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4* out);
 
 /* Ray-level query through the uploaded scene with subframe `subframe`'s TLAS:
  * rays are 8 floats (origin.xyz, dir.xyz, tmin, tmax).  For each ray, hits

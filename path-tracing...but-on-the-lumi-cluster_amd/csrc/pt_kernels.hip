@@ -1823,6 +1823,17 @@ int ptg_path_trace_samples(ptg_context* ctx, const ptg_render_config* cfg, size_
     return PTG_OK;
 }
 
+int ptg_tonemap_device(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4* out)
+{
+    if(int r = bind(ctx)) return r;
+    if(!n) return PTG_OK;
+    if(!color || !out || n >= (1u << 31)) return fail(PTG_E_INVALID, "ptg_tonemap_device: bad arguments");
+    hipLaunchKernelGGL(k_tonemap, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, uint32_t(n),
+                       reinterpret_cast<const float4*>(color), reinterpret_cast<uchar4*>(out));
+    PTG_HIP(hipGetLastError());
+    return PTG_OK;
+}
+
 int ptg_tonemap(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_uchar4* out)
 {
     if(int r = bind(ctx)) return r;

@@ -6,6 +6,15 @@ partitioned, never exchanged, except for one real step:
 
 * frames  - rank r renders its own frames (config 4: the animation,
             one frame per GPU).  No collective at all.
+* samples - one frame's sample range split into whole motion-blur groups
+            (8 samples, one subframe each) dealt to the ranks in order; each
+            rank renders every pixel over its range (ptg_render's
+            [sample_begin, sample_end)) and ONE sum-reduce of the float32
+            radiance to rank 0 assembles the frame (SURVEY 8(e)(ii),
+            `render_and_reduce`).  Not bit-identical: the reference sums the
+            samples of a pixel in index order in float32 (main.cc:24-39), and
+            a sum of per-range partial sums rounds differently (~1e-7
+            relative; tests/test_gpu_distributed.py measures it).
 * tiles   - one frame split into tile_w x tile_h tiles dealt round-robin to
             the ranks (tile t -> rank t % world; interleaving balances the
             up-to-7x per-pixel cost differences of a frame).  Each rank
@@ -152,6 +161,84 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
                 n = shard.count_for(r)
                 if n:
                     renderer.scatter_tiles(cfg, shard.tile_w, shard.tile_h, r, shard.world, n, part, image)
+    return image
+
+
+@dataclass
+class SampleShard:
+    """The sample range [j0, j1) of one rank: whole groups of `group` samples
+    (SAMPLES_PER_MOTION_BLUR_STEP, one subframe each), consecutive groups per
+    rank, as even as the group count allows."""
+    spp: int
+    rank: int
+    world: int
+    group: int
+
+    def __init__(self, cfg, rank, world, group=None):
+        self.spp = int(cfg.samples_per_pixel)
+        self.rank, self.world = int(rank), int(world)
+        self.group = int(group or getattr(cfg, "samples_per_motion_blur_step", 8) or 8)
+
+    def range_for(self, rank):
+        groups = -(-self.spp // self.group)
+        g0, g1 = rank * groups // self.world, (rank + 1) * groups // self.world
+        return min(self.spp, g0 * self.group), min(self.spp, g1 * self.group)
+
+    @property
+    def j0(self):
+        return self.range_for(self.rank)[0]
+
+    @property
+    def j1(self):
+        return self.range_for(self.rank)[1]
+
+
+def render_and_reduce(renderer, cfg, shard: SampleShard, image, accum=None, stream=None, force_collective=True):
+    """Render this rank's sample range of every pixel and sum-reduce the
+    radiance to rank 0, which tonemaps it into `image` (and copies the reduced
+    radiance into `accum` if given).  Each rank's partial is its range's
+    j-ordered float32 sum / SPP (ptg_render over [j0, j1)); rank 0 gets the
+    sum of the partials, so the frame is within float32 rounding of the
+    single-GPU render, not bit-identical to it (module docstring).
+
+    Like render_and_gather: everything is issued on `stream`, the collective
+    runs when the shard describes this process's place in the default group
+    (at world size 1 too, with `force_collective`), and a mismatch raises on
+    the rank that has it.  RCCL reduces the device tensors over xGMI; gloo
+    (CPU groups: tests, rehearsals) reduces through host memory."""
+    import contextlib
+
+    import torch
+    import torch.distributed as dist
+    dev = image.device
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped and dist.get_world_size() == shard.world and dist.get_rank() == shard.rank:
+        collective = shard.world > 1 or force_collective
+    elif shard.world == 1:
+        collective = False
+    elif not grouped:
+        raise RuntimeError("render_and_reduce: world size %d but no process group" % shard.world)
+    else:
+        raise RuntimeError("render_and_reduce: shard (rank %d of %d) does not match the process group (rank %d of %d)"
+                           % (shard.rank, shard.world, dist.get_rank(), dist.get_world_size()))
+    ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
+    with ctx:
+        h, w = image.shape[0], image.shape[1]
+        part = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+        if shard.j1 > shard.j0:
+            renderer.render(cfg, samples=(shard.j0, shard.j1), out_accum=part)
+        if collective:
+            if dist.get_backend() == "gloo":   # CPU process groups: reduce through host memory
+                host = part.cpu()
+                dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+                if shard.rank == 0:
+                    part.copy_(host)
+            else:                              # RCCL over xGMI: one sum-reduce of the radiance to rank 0
+                dist.reduce(part, dst=0, op=dist.ReduceOp.SUM)
+        if shard.rank == 0:
+            renderer.tonemap_device(part, image)
+            if accum is not None:
+                accum.copy_(part)
     return image
 
 

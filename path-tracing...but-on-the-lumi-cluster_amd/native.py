@@ -113,6 +113,7 @@ def lib():
         "ptg_scatter_tiles": (I, [P, P, U32, U32, U32, U32, U32, P, P]),
         "ptg_path_trace_samples": (I, [P, P, SZ, P, P, P]),
         "ptg_tonemap": (I, [P, SZ, P, P]),
+        "ptg_tonemap_device": (I, [P, SZ, P, P]),
         "ptg_trace_rays": (I, [P, U32, SZ, P, P]),
         "ptg_counters_enable": (I, [P, I]),
         "ptg_last_counters": (I, [P, P]),

@@ -130,6 +130,14 @@ class GpuRenderer:
                 "ptg_trace_rays")
         return hits
 
+    def tonemap_device(self, colors, out_bgra):
+        """tonemap_pixel over a device float32 [..., 4] tensor into a device
+        uint8 [..., 4] tensor (ptg_tonemap_device; asynchronous)."""
+        n = colors.numel() // 4
+        assert out_bgra.numel() == 4 * n
+        N.check(N.lib().ptg_tonemap_device(self._ctx, n, _ptr(colors), _ptr(out_bgra)), "ptg_tonemap_device")
+        return out_bgra
+
     def tonemap(self, colors: np.ndarray) -> np.ndarray:
         c = np.zeros((colors.shape[0], 4), np.float32)
         c[:, :colors.shape[1]] = colors[:, :4] if colors.shape[1] >= 4 else colors

@@ -147,3 +147,87 @@ def test_render_and_gather_shard_group_mismatch(tmp_path):
     mp.spawn(_mismatch_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
         assert np.load(out % r).tolist() == [True, True]
+
+
+# ---- sample-range shard ------------------------------------
+
+@pytest.mark.parametrize("spp,world", [(1024, 8), (1024, 3), (8, 2), (40, 3), (12, 2)])
+def test_sample_ranges_partition_whole_groups(spp, world):
+    """Every sample index lands on exactly one rank, in consecutive ranges of
+    whole motion-blur groups (8 samples, one subframe each)."""
+    cfg = N.RenderConfig.make(64, 32, spp)
+    seen = []
+    for r in range(world):
+        s = D.SampleShard(cfg, r, world)
+        assert s.j0 <= s.j1 and (s.j0 % 8 == 0) and (s.j1 % 8 == 0 or s.j1 == spp)
+        seen.extend(range(s.j0, s.j1))
+    assert seen == list(range(spp))
+
+
+class StubSampleRenderer:
+    """Stands in for GpuRenderer on CPU: render over a sample range writes the
+    range's sum of f(x, y, j) / SPP (float32), tonemap_device a byte function
+    of the radiance."""
+
+    def __init__(self):
+        self.calls = []
+
+    @staticmethod
+    def f(x, y, j):
+        return np.float32(1e-3) * np.float32((x * 7 + y * 13 + j * 3) % 97)
+
+    def render(self, cfg, samples=None, out_accum=None, **_):
+        j0, j1 = samples
+        self.calls.append(("render", j0, j1))
+        h, w = out_accum.shape[:2]
+        yy, xx = np.mgrid[0:h, 0:w]
+        acc = np.zeros((h, w), np.float32)
+        for j in range(j0, j1):
+            acc += self.f(xx, yy, j)
+        acc /= np.float32(cfg.samples_per_pixel)
+        out_accum[..., 0] = torch.from_numpy(acc)
+        out_accum[..., 1] = torch.from_numpy(acc * 2)
+        out_accum[..., 2] = torch.from_numpy(acc * 3)
+        return None, out_accum
+
+    def tonemap_device(self, colors, out_bgra):
+        self.calls.append(("tonemap",))
+        out_bgra[..., 0] = (colors[..., 0] * 1000).to(torch.uint8)
+        out_bgra[..., 3] = 255
+        return out_bgra
+
+
+def _reduce_worker(rank, world, port, spp, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = N.RenderConfig.make(30, 20, spp)
+    shard = D.SampleShard(cfg, rank, world)
+    image = torch.zeros((20, 30, 4), dtype=torch.uint8)
+    accum = torch.zeros((20, 30, 4), dtype=torch.float32)
+    stub = StubSampleRenderer()
+    D.render_and_reduce(stub, cfg, shard, image, accum=accum)   # the product function, collective included
+    if rank == 0:
+        np.save(out, accum.numpy())
+        assert stub.calls == [("render", shard.j0, shard.j1), ("tonemap",)]
+        assert (image[..., 3] == 255).all()
+    else:
+        assert stub.calls == [("render", shard.j0, shard.j1)]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_reduce_assembles_radiance_gloo(tmp_path, world):
+    """render_and_reduce over a real gloo group: rank 0 holds the sum of every
+    rank's range, which equals the whole-range sum within float32 rounding."""
+    spp = 48
+    out = str(tmp_path / "acc.npy")
+    mp.spawn(_reduce_worker, args=(world, _free_port(), spp, out), nprocs=world, join=True)
+    acc = np.load(out)
+    yy, xx = np.mgrid[0:20, 0:30]
+    want = np.zeros((20, 30), np.float64)
+    for j in range(spp):
+        want += StubSampleRenderer.f(xx, yy, j).astype(np.float64)
+    want /= spp
+    assert np.allclose(acc[..., 0], want, rtol=1e-5, atol=1e-7)
+    assert np.allclose(acc[..., 2], 3 * want, rtol=1e-5, atol=1e-7)

@@ -12,6 +12,9 @@ for f in ("device/path_tracer.h", "device/block_format.h", "device/wavefront.h",
 # entry points the current C ABI declares but the old sources lack: stubs (timing builds only)
 p = os.path.join(sys.argv[1], "pt_kernels.hip")
 s = open(p).read()
-if "ptg_arith_selftest" not in s:
-    s += '\nextern "C" int ptg_arith_selftest(ptg_context*) { return 0; }\n'
-    open(p, "w").write(s)
+stubs = {"ptg_arith_selftest": 'extern "C" int ptg_arith_selftest(ptg_context*) { return 0; }',
+         "ptg_tonemap_device": 'extern "C" int ptg_tonemap_device(ptg_context*, size_t, const ptg_float4*, ptg_uchar4*) { return -1; }'}
+for name, body in stubs.items():
+    if name not in s:
+        s += "\n" + body + "\n"
+open(p, "w").write(s)
