@@ -18,7 +18,10 @@ cd "$W"
 /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
   -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I"$R/include" -I. "$@" -c pt_kernels.hip -o "$OUT/pt_kernels.o"
 HOST_OBJS=$(echo "$PKG"/_build/obj/{mesh_loader,bvh_builder,host_trace,scene,block_bvh}.o)
-if [ -n "$HOST_FLAGS" ]; then   # the variant changes the host side too (e.g. -DPTG_BLOCK_WIDTH=8): rebuild it
+# the variant changes the host side too (e.g. -DPTG_BLOCK_WIDTH=8, or a whole
+# commit's sources: at_commit.py writes .rebuild_host): rebuild it from the
+# scratch copy, never mix the shipped packer with other walker sources
+if [ -n "$HOST_FLAGS" ] || [ -f "$W/.rebuild_host" ]; then
   HOST_OBJS=""
   for f in mesh_loader bvh_builder host_trace scene block_bvh; do
     g++ -std=c++17 -O2 -fPIC -ffp-contract=off -fno-fast-math -I"$R/include" -I"$PKG/_gen" -I. -pthread $HOST_FLAGS \
