@@ -221,6 +221,10 @@ __global__ __launch_bounds__(kBlock) void k_wf_camera(DevScene sc, PixelMap pm, 
 // the grid is sized to what is resident, each wave owns a contiguous range of
 // the queue (no atomics), and a lane that finishes its ray takes the next one
 // of its wave's range, so the wave never idles behind its longest ray.
+#ifndef PTG_ANY_RUN
+#define PTG_ANY_RUN 4
+#endif
+constexpr uint32_t kAnyRun = PTG_ANY_RUN;   // consecutive queue groups per run of the any-hit walk (k_wf_walk)
 constexpr int kRefillIdle = 24;   // refill once at least this many lanes are idle (16 / 32: slower)
 // waves per SIMD the walks are compiled for: the closest-hit walk at 96 VGPRs
 // (104 uncapped, no spills at 96), the any-hit walk at 80 (76 used), so a
@@ -270,7 +274,14 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     const uint32_t groups = (n + 63u) >> 6;
     const uint32_t band = max(1u, (groups + kBands - 1u) / kBands);
     const uint32_t local = (kBands / nxcd) * band;    // this XCD's group slots (some past the end)
-    const uint32_t end = wave < local ? ((local - wave + waves - 1) / waves) * 64u : 0u;
+    // The any-hit walk deals runs of kAnyRun consecutive groups per wave (wave
+    // w: runs w, w + W, ...) instead of single groups: a wave's next group is
+    // then usually the same pixels' next 8 samples (or the next pixels), so
+    // the occluder its last group found (the candidate, try_candidate) lies on
+    // the new rays' way to the sun too.  The closest-hit walk keeps runs of 1.
+    constexpr uint32_t R = ANY ? kAnyRun : 1u;
+    const uint32_t runs = (local + R - 1u) / R;
+    const uint32_t end = wave < runs ? ((runs - wave + waves - 1) / waves) * R * 64u : 0u;
     uint32_t cursor = 0;
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
     const float tmax = ANY ? MAX_RAY_DIST : 1e9f;
@@ -323,9 +334,10 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                 if(!active)
                 {
                     const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                    const uint32_t l = wave + (v >> 6) * waves;
+                    const uint32_t k = v >> 6;   // this wave's k-th group
+                    const uint32_t l = (wave + (k / R) * waves) * R + k % R;
                     const uint32_t t = ((xcd + nxcd * (l / band)) * band + l % band) * 64u + (v & 63u);
-                    if(v < end && t < n)
+                    if(v < end && l < local && t < n)
                     {
                         q = ANY ? list[t] : t;
 #if PTG_DEBUG

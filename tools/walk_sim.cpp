@@ -861,15 +861,17 @@ int main(int argc, char** argv)
         // instance level: the candidate instance's BLAS walked first
         {
             const char* in_names[] = {"Pi (path)", "Wi (wave, last)", "Xi (pixel)", "Pi else Wi", "Pi else Xi else Wi",
-                                      "(P else W) tri+inst", "(W) tri+inst"};
-            const int NI = 7;
+                                      "(P else W) tri+inst", "(W) tri+inst", "(G prev group) tri+inst"};
+            const int NI = 8;
             double cost[NI] = {}, have_i[NI] = {}, hit_i[NI] = {};
             for(int r = 0; r < 4; ++r)
             {
                 std::map<uint32_t, uint32_t> pix;
+                uint32_t group_last = 0xFFFFFFFFu, group_last_p = 0xFFFFFFFFu;   // the previous group's last occluder
                 for(uint32_t w = 0; w < nwaves; ++w)
                 {
                     uint32_t wave_last = 0xFFFFFFFFu, wave_last_p = 0xFFFFFFFFu;
+                    const uint32_t prev_g = group_last, prev_gp = group_last_p;
                     for(uint32_t l = 0; l < 64; ++l)
                     {
                         const SQ& x = sq[r][size_t(w) * 64 + l];
@@ -883,8 +885,8 @@ int main(int argc, char** argv)
                         if(auto it = pix.find(x.pixel); it != pix.end()) xc = it->second;
                         const uint32_t cand[NI] = {pc, wave_last, xc, pc != ~0u ? pc : wave_last,
                                                    pc != ~0u ? pc : (xc != ~0u ? xc : wave_last),
-                                                   pc != ~0u ? pc : wave_last, wave_last};
-                        const uint32_t cprim[NI] = {~0u, ~0u, ~0u, ~0u, ~0u, pc != ~0u ? pp : wave_last_p, wave_last_p};
+                                                   pc != ~0u ? pc : wave_last, wave_last, prev_g};
+                        const uint32_t cprim[NI] = {~0u, ~0u, ~0u, ~0u, ~0u, pc != ~0u ? pp : wave_last_p, wave_last_p, prev_gp};
                         for(int pi = 0; pi < NI; ++pi)
                         {
                             if(cand[pi] == ~0u) { cost[pi] += x.steps; continue; }
@@ -896,6 +898,7 @@ int main(int argc, char** argv)
                         }
                         if(x.occ) { wave_last = x.oi; wave_last_p = x.op; pix[x.pixel] = x.oi; }
                     }
+                    if(wave_last != ~0u) { group_last = wave_last; group_last_p = wave_last_p; }
                 }
             }
             for(int pi = 0; pi < NI; ++pi)
