@@ -1116,14 +1116,15 @@ int main(int argc, char** argv)
         // node phase, leaf phase only when >= T lanes want one (or no lane
         // can take a node step).
         const double kRows = (28.0 * kBlockWidth + 15) / 16;   // 16-byte rows a block step reads (7 at width 4)
-        int U = 2, K = 1, T = 1, R = 24;
-        sscanf(ls, "%d %d %d %d", &U, &K, &T, &R);
+        int U = 2, K = 1, T = 1, R = 24, E = 1;   // E: BLAS entries only in every E-th leaf phase
+        sscanf(ls, "%d %d %d %d %d", &U, &K, &T, &R, &E);
         for(int any = 0; any < 2; ++any)
         {
             std::vector<const Query*> mine;
             for(const Query& q: qs)
                 if(q.any == bool(any)) mine.push_back(&q);
             double ni = 0, nl = 0, li = 0, ll = 0, ri = 0, rl = 0, phases = 0, iters = 0, waves = 0, act = 0, leaf_ph = 0, leaf_ph_enter = 0, rph = 0;
+            double leaf_ph_tri = 0;
             const size_t per_wave = 4096;   // queries one wave works through (its range)
             uint64_t lmism = 0;
             double why[5] = {};   // node-phase lanes not reading a block: instance leaf, triangle leaf, parked & waiting, popped nothing steppable, empty
@@ -1171,19 +1172,23 @@ int main(int argc, char** argv)
                     int want = 0, can_node = 0;
                     for(auto& l: lane)
                         if(l) { want += l->wants_leaf() ? 1 : 0; can_node += l->at_leaf() ? 0 : 1; }
+                    const bool entry_phase = E <= 1 || (uint64_t(iters) % uint64_t(E)) == 0;
                     if(want && (want >= T || can_node == 0 || want == live))
                     {
-                        int loads = 0, enters = 0;
+                        int loads = 0, enters = 0, tris = 0;
                         for(auto& l: lane)
                         {
                             if(!l || !l->wants_leaf()) continue;
+                            if(!entry_phase && l->axis < 0 && l->pend == kBePop) continue;   // its BLAS entry waits
+                            const double t0 = l->st.tri;
                             const double before = l->st.tri + l->st.enters, e0 = l->st.enters;
                             const int r = l->leaf_step();
                             loads += (l->st.tri + l->st.enters > before) ? 1 : 0;
                             enters += (l->st.enters > e0) ? 1 : 0;
+                            tris += (l->st.tri > t0) ? 1 : 0;
                             if(r) { check(*l); l.reset(); }
                         }
-                        if(loads) { li += 4; ll += 4 * loads; phases++; leaf_ph++; leaf_ph_enter += enters ? 1 : 0; }
+                        if(loads) { li += 4; ll += 4 * loads; phases++; leaf_ph++; leaf_ph_enter += enters ? 1 : 0; leaf_ph_tri += tris ? 1 : 0; }
                     }
                 }
             }
@@ -1197,6 +1202,8 @@ int main(int argc, char** argv)
             printf("  refill phases %.2f per wave-query64 (R=%d)\n", rph * 64 / nq, R);
             printf("  leaf phases with a BLAS entry: %.1f%%; %llu mismatches vs the link walk\n",
                    100.0 * leaf_ph_enter / std::max(leaf_ph, 1.0), (unsigned long long)lmism);
+            printf("  per 64 queries: %.1f iterations, %.1f node phases with loads, %.1f leaf phases with an entry, %.1f with a triangle (E=%d)\n",
+                   iters * 64 / nq, ni / kRows * 64 / nq, leaf_ph_enter * 64 / nq, leaf_ph_tri * 64 / nq, E);
         }
         return 0;
     }
