@@ -2,6 +2,7 @@
 // link orders (bvh.cc:145-229) -> 4-wide blocks, breadth-first, so the top
 // levels every ray walks share cache lines.
 #include "block_bvh.h"
+#include "hmath.h"
 #include <algorithm>
 #include <cstring>
 #include <thread>
@@ -272,6 +273,35 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
 } // namespace ptg
 
 namespace ptg {
+
+bool leaf_boxes_are_vertex_bounds(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count,
+                                  const uint32_t* indices, size_t index_count, const ptg_float3* pos, size_t vertex_count,
+                                  uint32_t index_offset, uint32_t triangle_count, uint32_t base_vertex_offset)
+{
+    for(uint32_t n = 0; n < count; ++n)
+    {
+        const ptg_bvh_link& l = links[n];   // octant 0's order
+        if(!(l.accept & 0x80000000u)) continue;
+        const uint32_t t = l.accept & 0x7FFFFFFFu;
+        const size_t i0 = size_t(index_offset) + 3 * size_t(t);
+        if(t >= triangle_count || i0 + 3 > index_count) return false;
+        const ptg_float3* P[3];
+        for(int k = 0; k < 3; ++k)
+        {
+            const size_t v = size_t(base_vertex_offset) + indices[i0 + k];
+            if(v >= vertex_count) return false;
+            P[k] = pos + v;
+        }
+        using hm::fminf_;
+        using hm::fmaxf_;
+        const float lo[3] = {fminf_(P[0]->x, fminf_(P[1]->x, P[2]->x)), fminf_(P[0]->y, fminf_(P[1]->y, P[2]->y)),
+                             fminf_(P[0]->z, fminf_(P[1]->z, P[2]->z))};
+        const float hi[3] = {fmaxf_(P[0]->x, fmaxf_(P[1]->x, P[2]->x)), fmaxf_(P[0]->y, fmaxf_(P[1]->y, P[2]->y)),
+                             fmaxf_(P[0]->z, fmaxf_(P[1]->z, P[2]->z))};
+        if(memcmp(lo, &nodes[n].min_x, 12) != 0 || memcmp(hi, &nodes[n].max_x, 12) != 0) return false;
+    }
+    return true;
+}
 
 // The subframes' TLASes are built over nearly the same instances (only the
 // moving ones differ), so most of their subtrees are identical: ~98% of the

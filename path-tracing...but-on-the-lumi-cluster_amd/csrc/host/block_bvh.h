@@ -34,6 +34,20 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
 
 namespace ptg {
 
+// Whether every leaf box of a BLAS (nodes[0..count), links in the reference
+// layout) is exactly the bounds of its triangle's three positions as the
+// reference's builder computes them (bvh.cc:243-246: fmin / fmax, the float
+// overloads, whose tie rule fixes the sign of zero bounds) - the any-hit
+// walk tests a candidate triangle's leaf box from its vertices
+// (BlockWalker::try_candidate).  `indices` and `pos` are the scene's arrays;
+// the mesh is (index_offset, triangle_count, base_vertex_offset).  Built by
+// the host compiler with the builder's flags (host/hmath.h), so the
+// comparison is bit for bit: hipcc's std::fmin (llvm.minnum) may pick either
+// zero of a +0 / -0 tie.
+bool leaf_boxes_are_vertex_bounds(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count,
+                                  const uint32_t* indices, size_t index_count, const ptg_float3* pos, size_t vertex_count,
+                                  uint32_t index_offset, uint32_t triangle_count, uint32_t base_vertex_offset);
+
 // A packed BLAS in the block cache.
 struct BlasRecord {
     uint32_t root = 0;          // root block

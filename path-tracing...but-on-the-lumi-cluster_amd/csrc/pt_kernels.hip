@@ -1573,32 +1573,12 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
         const auto key = std::make_tuple(in.blas.node_offset, in.m.index_offset, in.m.base_vertex_offset);
         auto it = ctx->leaf_bounds_ok.find(key);
         if(it != ctx->leaf_bounds_ok.end()) return it->second;
-        bool ok = true;
-        for(uint32_t n = 0; ok && n < in.blas.node_count; ++n)
-        {
-            const ptg_bvh_link& l = ctx->host_links[size_t(in.blas.node_offset) * 8 + n];   // octant 0's order
-            if(!(l.accept & 0x80000000u)) continue;
-            const uint32_t t = l.accept & 0x7FFFFFFFu;
-            const size_t i0 = size_t(in.m.index_offset) + 3 * size_t(t);
-            if(t >= in.m.triangle_count || i0 + 2 >= ctx->host_indices.size()) { ok = false; break; }
-            float lo[3], hi[3];
-            const ptg_float3* P[3];
-            for(int k = 0; k < 3; ++k)
-            {
-                const size_t v = size_t(in.m.base_vertex_offset) + ctx->host_indices[i0 + k];
-                if(v >= ctx->host_pos.size()) { ok = false; break; }
-                P[k] = &ctx->host_pos[v];
-            }
-            if(!ok) break;
-            lo[0] = std::fmin(P[0]->x, std::fmin(P[1]->x, P[2]->x));
-            lo[1] = std::fmin(P[0]->y, std::fmin(P[1]->y, P[2]->y));
-            lo[2] = std::fmin(P[0]->z, std::fmin(P[1]->z, P[2]->z));
-            hi[0] = std::fmax(P[0]->x, std::fmax(P[1]->x, P[2]->x));
-            hi[1] = std::fmax(P[0]->y, std::fmax(P[1]->y, P[2]->y));
-            hi[2] = std::fmax(P[0]->z, std::fmax(P[1]->z, P[2]->z));
-            const ptg_bvh_node& nd = ctx->host_nodes[size_t(in.blas.node_offset) + n];
-            ok = memcmp(lo, &nd.min_x, 12) == 0 && memcmp(hi, &nd.max_x, 12) == 0;
-        }
+        // (host code built by the host compiler with the builder's flags:
+        // fmin / fmax with the reference's tie rule, host/block_bvh.cpp)
+        const bool ok = leaf_boxes_are_vertex_bounds(
+            ctx->host_nodes.data() + in.blas.node_offset, ctx->host_links.data() + size_t(in.blas.node_offset) * 8,
+            in.blas.node_count, ctx->host_indices.data(), ctx->host_indices.size(), ctx->host_pos.data(),
+            ctx->host_pos.size(), in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset);
         ctx->leaf_bounds_ok[key] = ok;
         return ok;
     };

@@ -33,6 +33,9 @@ def test_block_walk_matches_link_walk(walk_sim, assets_dir, frame):
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
     assert m and int(m.group(1)) > 5000 and int(m.group(2)) == 0, r.stdout
+    # the any-hit candidates' requirement (a candidate's leaf box is tested from its vertices)
+    lb = re.search(r"instances whose BLAS leaf boxes are not their vertex bounds: (\d+) of (\d+)", r.stdout)
+    assert lb and int(lb.group(1)) == 0 and int(lb.group(2)) > 100, r.stdout
     # the block walk takes about half the dependent steps of the link walk
     steps = [float(x) for x in re.findall(r"steps ([0-9.]+)", r.stdout)]
     link_closest, block_closest = steps[0], steps[1]
@@ -65,3 +68,26 @@ def test_eight_wide_blocks_exact(native_lib, assets_dir):
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
     assert m and int(m.group(2)) == 0, r.stdout
+
+
+def test_zero_and_nan_direction_components(walk_sim, assets_dir):
+    """A ray with a zero direction component (1/dir infinite) takes the
+    walk's min/max form of the slab test (BlockWalker::node_block).  Bounces
+    with one or two zero components, the sun's exact direction (which has one
+    in this scene) and NaN directions return the reference's hits, with about
+    as many steps as the other rays."""
+    env = dict(os.environ, AXIS="1")
+    r = subprocess.run([walk_sim, assets_dir, "450", "3000", "16"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    z = re.search(r"queries with a zero direction component: (\d+) of (\d+)", r.stdout)
+    assert z and int(z.group(1)) > int(z.group(2)) // 10, r.stdout
+    m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
+    assert m and int(m.group(2)) == 0, r.stdout
+    steps = [float(x) for x in re.findall(r"steps ([0-9.]+)", r.stdout)]
+    assert steps[3] < 0.7 * steps[2], r.stdout   # shadow rays: block walk vs link walk
+    # NaN directions (one, two or three components) are in the mix too: a ray
+    # with three NaN components passes no box, one with one or two is tested
+    # on its other axes as in the reference (which enters more BLASes for
+    # them), so no query walks the whole scene (580k nodes)
+    mx = re.search(r"most block-walk steps of one query: (\d+)", r.stdout)
+    assert mx and int(mx.group(1)) < 10000, r.stdout

@@ -39,6 +39,8 @@ if a.counters:
     extra = {k: {n: int(v[i]) for i, n in enumerate(names)} for k, v in kc.items() if int(v[:8].sum())}
     if a.pipeline == "wavefront":
         extra["redo"] = r.redo_stats()
-print(json.dumps({"counters": extra, "lib": os.path.basename(N.LIB_PATH), "pipeline": a.pipeline, "spp": a.spp, "bounces": a.bounces,
+import hashlib, numpy as np
+sha_bgra = hashlib.sha256(np.ascontiguousarray(img.cpu().numpy(), np.uint8).tobytes()).hexdigest()[:32]
+print(json.dumps({"sha_bgra": sha_bgra, "counters": extra, "lib": os.path.basename(N.LIB_PATH), "pipeline": a.pipeline, "spp": a.spp, "bounces": a.bounces,
                   "frame": a.frame, "wall_ms": round(best, 2), "msamples_per_s": round(a.width * a.height * a.spp / best / 1e3, 2),
                   "kernels_ms": {k: round(v[0], 2) for k, v in kt.items() if v[1]}}))

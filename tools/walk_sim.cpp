@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
 #include <memory>
 #include <set>
@@ -433,9 +434,12 @@ struct SimWalker {
     }
 };
 
+double g_max_query_steps = 0;   // the most block-walk steps any query took
+
 Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats& st, uint32_t C)
 {
     st.queries++;
+    const double steps0 = st.steps;
     SimWalker w(v, pk, q, st, C, g_spec);
     static const int sched = getenv("SCHED") ? atoi(getenv("SCHED")) : 0;
     for(;;)
@@ -456,6 +460,7 @@ Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats&
         st.iters++;
     }
     st.depth_hist[w.maxd]++;
+    g_max_query_steps = std::max(g_max_query_steps, st.steps - steps0);
     g_last_split[0] = w.tl_steps;
     g_last_split[1] = w.blas_cur;
     g_last_split[2] = w.enters_n;
@@ -528,6 +533,19 @@ int main(int argc, char** argv)
     pk.E.insert(pk.E.end(), fp.tlas.begin(), fp.tlas.end());
     pk.inst_root = fp.inst_root;
     pk.tlas_root = fp.tlas_root;
+    {   // the any-hit candidates' requirement (the upload checks it per BLAS and mesh)
+        ptg_scene_view w;
+        ptg_scene_view_get(scene, &w);
+        size_t bad = 0;
+        for(size_t i = 0; i < w.instance_count; ++i)
+        {
+            const ptg_tlas_instance& in = w.instances[i];
+            bad += leaf_boxes_are_vertex_bounds(w.nodes + in.blas.node_offset, w.links + size_t(in.blas.node_offset) * 8,
+                                                in.blas.node_count, w.indices, w.index_count, w.pos, w.vertex_count,
+                                                in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset) ? 0 : 1;
+        }
+        printf("instances whose BLAS leaf boxes are not their vertex bounds: %zu of %zu\n", bad, w.instance_count);
+    }
     printf("frame %u: BLAS %zu + %zu new copies (%.1f MB), TLAS %zu copies (%.1f MB); stack bound %u entries (TLAS %u)\n",
            frame, cache.blas.size(), fp.new_blas.size(), (cache.blas.size() + fp.new_blas.size()) * 128 / 1e6, fp.tlas.size(),
            fp.tlas.size() * 128 / 1e6, fp.stack_bound(), fp.tlas_stack);
@@ -947,10 +965,32 @@ int main(int argc, char** argv)
             qs.push_back(Query{o, L, 1e-4f, 1e9f, sf, true, bnc, src});
             f3 nd;
             do { nd = v3(rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1); } while(dot(nd, nd) > 1 || dot(nd, nd) < 1e-4f);
+            static const bool axis_dirs = getenv("AXIS") != nullptr;   // bounces with zero / NaN direction components
+            if(axis_dirs && rnd() < 0.02f)
+            {   // a NaN direction (one, two or all three components), as a degenerate shading frame makes
+                const float qn = std::numeric_limits<float>::quiet_NaN();
+                f3 bad = nd;
+                const int k = int(rnd() * 3) % 3, cnt = 1 + int(rnd() * 3) % 3;
+                for(int c = 0; c < cnt; ++c) ((k + c) % 3 == 0 ? bad.x : (k + c) % 3 == 1 ? bad.y : bad.z) = qn;
+                qs.push_back(Query{o, bad, 1e-4f, 1e9f, sf, false, bnc, src});
+                qs.push_back(Query{o, bad, 1e-4f, 1e9f, sf, true, bnc, src});
+            }
+            if(axis_dirs && rnd() < 0.5f)
+            {   // one or two components exactly zero (1/dir infinite: the walk's min/max form)
+                const int k = int(rnd() * 3) % 3;
+                (k == 0 ? nd.x : k == 1 ? nd.y : nd.z) = 0.0f;
+                if(rnd() < 0.3f) (k == 0 ? nd.y : k == 1 ? nd.z : nd.x) = 0.0f;
+                if(dot(nd, nd) < 1e-4f) nd = v3(0, 1, 0);
+            }
             nd = normalize(nd);
             if(dot(nd, d) > 0) nd = -nd;
             d = nd;
         }
+    }
+    {
+        size_t zero = 0;
+        for(const Query& q: qs) zero += (q.d.x == 0.0f || q.d.y == 0.0f || q.d.z == 0.0f) ? 1 : 0;
+        printf("queries with a zero direction component: %zu of %zu\n", zero, qs.size());
     }
     if(const char* cs = getenv("CACHESIM"))
     {   // Cache behaviour of the walk kernel's access stream on one slice of
@@ -1222,6 +1262,7 @@ int main(int argc, char** argv)
         }
     }
     printf("%zu queries, %llu mismatches\n", qs.size(), (unsigned long long)mism);
+    printf("most block-walk steps of one query: %.0f\n", g_max_query_steps);
     for(int k = 0; k < 2; ++k)
     {
         const Stats& a = sl[k];
