@@ -1253,6 +1253,24 @@ int main(int argc, char** argv)
     {
         Res a = link_walk(v, q, sl[q.any]);
         Res b = block_walk(v, pk, q, sb[q.any], S);
+        if(getenv("CLOSEBOUND") && !q.any && b.inst != 0xFFFFFFFFu)
+        {   // model: the closest-hit walk started with tmax = next float above the
+            // final hit's t (a perfect neighbour candidate); same result, fewer steps?
+            static Stats cb, base;
+            static uint64_t nq = 0, wrong = 0;
+            Query q2 = q;
+            q2.tmax = std::nextafter(b.t, INFINITY);
+            Stats tmp;
+            const Res c = block_walk(v, pk, q2, cb, S);
+            block_walk(v, pk, q, base, S);
+            if(!(c == b) && wrong++ < 4)
+                fprintf(stderr, "  differ: t %a inst %u prim %u u %a | bounded t %a inst %u prim %u u %a\n", b.t, b.inst, b.prim, b.u,
+                        c.t, c.inst, c.prim, c.u);
+            if(++nq % 20000 == 0 || nq == 1)
+                fprintf(stderr, "CLOSEBOUND: %llu hit queries, %llu differ; block steps %.2f -> %.2f, box tests %.1f -> %.1f\n",
+                        (unsigned long long)nq, (unsigned long long)wrong, base.block_steps / base.queries, cb.block_steps / cb.queries,
+                        base.visits / base.queries, cb.visits / cb.queries);
+        }
         if(!(a == b))
         {
             if(mism < 5)
