@@ -36,6 +36,7 @@ def test_block_walk_matches_link_walk(walk_sim, assets_dir, frame):
     # the any-hit candidates' requirement (a candidate's leaf box is tested from its vertices)
     lb = re.search(r"instances whose BLAS leaf boxes are not their vertex bounds: (\d+) of (\d+)", r.stdout)
     assert lb and int(lb.group(1)) == 0 and int(lb.group(2)) > 100, r.stdout
+    assert "leaf-box check rejects a perturbed box: yes" in r.stdout, r.stdout
     # the block walk takes about half the dependent steps of the link walk
     steps = [float(x) for x in re.findall(r"steps ([0-9.]+)", r.stdout)]
     link_closest, block_closest = steps[0], steps[1]

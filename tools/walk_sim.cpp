@@ -545,6 +545,23 @@ int main(int argc, char** argv)
                                                 in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset) ? 0 : 1;
         }
         printf("instances whose BLAS leaf boxes are not their vertex bounds: %zu of %zu\n", bad, w.instance_count);
+        {   // and the check rejects a box that is not: instance 0's BLAS with one leaf box's
+            // min_x lowered by one ulp, and with +0 / -0 swapped in a zero bound if it has one
+            const ptg_tlas_instance& in = w.instances[0];
+            std::vector<ptg_bvh_node> nodes(w.nodes + in.blas.node_offset, w.nodes + in.blas.node_offset + in.blas.node_count);
+            const ptg_bvh_link* links = w.links + size_t(in.blas.node_offset) * 8;
+            uint32_t leaf = 0;
+            while(leaf < in.blas.node_count && !(links[leaf].accept & 0x80000000u)) ++leaf;
+            bool rejects = leaf < in.blas.node_count;
+            if(rejects)
+            {
+                nodes[leaf].min_x = std::nextafter(nodes[leaf].min_x, -INFINITY);
+                rejects = !leaf_boxes_are_vertex_bounds(nodes.data(), links, in.blas.node_count, w.indices, w.index_count, w.pos,
+                                                        w.vertex_count, in.m.index_offset, in.m.triangle_count,
+                                                        in.m.base_vertex_offset);
+            }
+            printf("leaf-box check rejects a perturbed box: %s\n", rejects ? "yes" : "no");
+        }
     }
     printf("frame %u: BLAS %zu + %zu new copies (%.1f MB), TLAS %zu copies (%.1f MB); stack bound %u entries (TLAS %u)\n",
            frame, cache.blas.size(), fp.new_blas.size(), (cache.blas.size() + fp.new_blas.size()) * 128 / 1e6, fp.tlas.size(),
