@@ -1255,24 +1255,50 @@ PTG_D bool ray_sphere(f3 o, f3 d, f3 c, float radius, float& tmin, float& tmax)
 
 constexpr float RAY_R = 5.8e-6f, RAY_G = 13.6e-6f, RAY_B = 33.1e-6f, MIE_K = 4.0e-6f;
 
+// The prologue of nishita_atmosphere_attenuation (:456-497): whether the ray
+// misses the atmosphere (attenuation 1), its primary step length, and whether
+// one of its steps lies below the ground (attenuation exactly 0).  The
+// reference sums the depths over every step and then returns 0 if a step lay
+// below the ground; the sums are only read when none did, so the heights are
+// tested first and the exp work is skipped for a shadowed ray (the same
+// result; the heights are recomputed bit for bit).
+struct AttenSteps {
+    bool outside, blocked;
+    float segment;
+};
+PTG_D AttenSteps attenuation_steps(float jitter, f3 pos, f3 view, float tmax)
+{
+    const f3 earth = V3(0, -EARTH_RADIUS, 0);
+    AttenSteps a{false, false, 0.0f};
+    float tmin = 0, atmax = 0;
+    if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax))
+    {
+        a.outside = true;
+        return a;
+    }
+    tmin = (float)gmax_d((double)tmin, 0.0);
+    tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
+    a.segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
+    for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
+    {
+        const float t = a.segment * (jitter + (float)i);
+        if(length((pos + t * view) - earth) - EARTH_RADIUS < 0)
+        {
+            a.blocked = true;
+            return a;
+        }
+    }
+    return a;
+}
+
 // nishita_atmosphere_attenuation (:456-497)
 template<class MP> PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view, float tmax, MP& mp)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
-    float tmin = 0, atmax = 0;
-    if(!ray_sphere(pos, view, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, tmin, atmax)) return V3(1.0f, 1.0f, 1.0f);
-    tmin = (float)gmax_d((double)tmin, 0.0);
-    tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
-    const float segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
-    // The reference sums the depths over every step and then returns 0 if a
-    // step lay below the ground; the sums are only read when none did, so the
-    // heights are tested first and the exp work is skipped for a shadowed ray
-    // (the same result; the heights are recomputed bit for bit).
-    for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
-    {
-        const float t = segment * (jitter + (float)i);
-        if(length((pos + t * view) - earth) - EARTH_RADIUS < 0) return V3(0.0f, 0.0f, 0.0f);
-    }
+    const AttenSteps a = attenuation_steps(jitter, pos, view, tmax);
+    if(a.outside) return V3(1.0f, 1.0f, 1.0f);
+    if(a.blocked) return V3(0.0f, 0.0f, 0.0f);
+    const float segment = a.segment;
     float ray_depth = 0, mie_depth = 0;
     for(int i = 0; i < PRIMARY_ITERATIONS; ++i)
     {
@@ -1379,6 +1405,20 @@ template<class MP> PTG_D f3 nee_finish(const NeeCandidate& c, f3 pos, MP& mp)
 {
     const f3 color = c.color * atmosphere_attenuation(c.jitter, pos, c.dir, MAX_RAY_DIST, mp);
     return color / c.mis_pdf;
+}
+
+// Whether the shadow ray of a prepared NEE candidate can be left untraced:
+// when one step of the sun ray's atmosphere integral lies below the ground,
+// the attenuation is exactly 0 before any exp (attenuation_steps), and if
+// nee_finish's value, (colour * 0) / mis_pdf, is then +0 in every component,
+// it is bitwise the V3(0, 0, 0) an occluded ray gives: the next round adds
+// att * (+0) either way.  Only the occlusion test is skipped; the random
+// draws and every value are the reference's.
+PTG_D bool nee_shadow_moot(const NeeCandidate& c, f3 pos)
+{
+    if(!attenuation_steps(c.jitter, pos, c.dir, MAX_RAY_DIST).blocked) return false;
+    const f3 z = (c.color * V3(0.0f, 0.0f, 0.0f)) / c.mis_pdf;
+    return (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
 }
 
 template<bool COUNT, class SC>

@@ -196,7 +196,8 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     // bounce `round` (path_tracer.hh:699-720): NEE setup, BSDF sample, next ray
     const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
     const f3 view = tangent_view(p.ray_d, info);
-    const bool pending = nee_prepare(seed, L, info, M, view, p.nee, mp);
+    // a shadow ray whose outcome cannot change the result is not traced (nee_shadow_moot)
+    const bool pending = nee_prepare(seed, L, info, M, view, p.nee, mp) && !nee_shadow_moot(p.nee, info.pos);
     const f4 ub = uniform4(seed);
     f3 tdir, batt;
     float bpdf;
