@@ -980,6 +980,34 @@ int main(int argc, char** argv)
             f3 L = normalize(v.subframes[sf].light.direction);
             src = r.inst;
             qs.push_back(Query{o, L, 1e-4f, 1e9f, sf, true, bnc, src});
+            {   // model of the surface pass's untraced shadow rays (path_tracer.h attenuation_steps):
+                // the sun ray's atmosphere integral has a step below the ground (float arithmetic
+                // as the device's, the jitter drawn here)
+                static uint64_t n_sh = 0, n_blocked = 0;
+                const float R = 6.3781e6f, H = 1.0e5f;
+                const f3 oc = o - v3(0, -R, 0);
+                const float b = dot(oc, L), cc = dot(oc, oc) - (R + H) * (R + H);
+                float disc = b * b - cc;
+                bool blocked = false;
+                if(disc >= 0)
+                {
+                    disc = std::sqrt(disc);
+                    float tmin = -b - disc, tmax = -b + disc;
+                    tmin = float(std::max(double(tmin), 0.0));
+                    tmax = std::min(tmax, 1e9f);
+                    const float seg = (tmax - tmin) / 8.0f, jit = rnd();
+                    for(int i = 0; i < 8 && !blocked; ++i)
+                    {
+                        const f3 pp = o + L * (seg * (jit + float(i))) - v3(0, -R, 0);
+                        blocked = std::sqrt(dot(pp, pp)) - R < 0;
+                    }
+                }
+                ++n_sh;
+                n_blocked += blocked;
+                if((n_sh & (n_sh - 1)) == 0 && n_sh >= 1024)
+                    fprintf(stderr, "shadow rays whose sun ray is blocked by the ground: %.1f%% of %llu\n",
+                            100.0 * double(n_blocked) / double(n_sh), (unsigned long long)n_sh);
+            }
             f3 nd;
             do { nd = v3(rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1); } while(dot(nd, nd) > 1 || dot(nd, nd) < 1e-4f);
             static const bool axis_dirs = getenv("AXIS") != nullptr;   // bounces with zero / NaN direction components
