@@ -12,6 +12,14 @@
 // shadow ray toward the sun from every hit (the wavefront's query mix).
 //
 //   make -C tools walk_sim && tools/_bin/walk_sim <assets> <frame> [paths] [ring dwords]
+//
+// Environment switches (each a model experiment):
+//   AXIS=1        bounces with zero / NaN direction components in the mix
+//   CLOSEBOUND=1  closest-hit walks started with tmax just above their own hit
+//   OCC=1, ANYORDER, CLOSEORDER, ORDERLEVEL, LOCKSTEP, CACHESIM, PACKET, SPEC,
+//   NONEAR, SCHED   (see their blocks below)
+// It also prints the share of the mix's shadow rays whose sun ray is blocked
+// by the ground (the surface pass leaves those untraced, nee_shadow_moot).
 #include "ptg.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/block_bvh.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/hmath.h"
