@@ -618,7 +618,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MP::kFas
 // work end to end, and here glibc's restated exp (its table copied to LDS)
 // beats ocml's plus rounding certificates (MathFast: 2x the code, spills at
 // 5 waves; measured DESIGN.md section 4), so this pass is exact by itself.
-#define PTG_SKY_WAVES 4     // 112 VGPRs, no spills
+#define PTG_SKY_WAVES 5     // 96 VGPRs (10 spilled); 4 waves: 103, none - 5 measured 0.26% faster on frames 0 and 450 (profiles/r04q_tune/ab_sky5.log)
 template<bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PTG_SKY_WAVES, 8))) void k_wf_sky(
     DevScene sc, PathSoA cur, TraceOut tr, uint32_t round, const uint32_t* __restrict__ sky_list,
