@@ -423,7 +423,10 @@ def main():
     scene = N.Scene(assets, cfg)
     r = GpuRenderer(local)
     # the arithmetic environment the bit-exact results rest on (ptg_arith_selftest)
-    selftest = r.selftest()
+    try:
+        selftest = r.selftest()
+    except RuntimeError as e:   # a timing variant without the self-test (tools/variants/at_commit.py): never "passed"
+        selftest = "unavailable: %s" % e
     stream = torch.cuda.current_stream(local)
     r.set_stream(stream)
     r.set_concurrency(args.concurrency)

@@ -234,7 +234,11 @@ int ptg_tonemap_device(ptg_context* ctx, size_t n, const ptg_float4* color, ptg_
  * gets 8 words {bary.x, bary.y, bary.z, thit (f32), instance_id, primitive_id,
  * back_face, shadowed}: the closest hit of ray_query_proceed/confirm
  * (ray_query.hh:248-290) and the any-hit bool of a single proceed
- * (path_tracer.hh:415-427).  HOST pointers; synchronous. */
+ * (path_tracer.hh:415-427).  HOST pointers; synchronous.
+ * Contract: every tmin is +0 or positive (or NaN / +inf, which no hit
+ * passes), as the reference's queries are (0 and MIN_RAY_DIST); a ray with a
+ * negative or -0 tmin is refused (PTG_E_INVALID, nothing traced).  Any tmax
+ * is accepted. */
 int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* rays, uint32_t* hits);
 
 /* Work counters of the last ptg_render* call (filled only while counting is

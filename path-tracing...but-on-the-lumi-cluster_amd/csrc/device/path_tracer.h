@@ -239,6 +239,7 @@ struct PrivStack {
     PTG_D void reserve(uint32_t) {}
     PTG_D void put(uint2 e, bool keep) { v[sp] = e; sp += keep ? 1u : 0u; }
     PTG_D uint2 pop() { return v[--sp]; }
+    PTG_D bool fits(uint32_t n, uint32_t stride) const { return sp + n <= stride; }
 };
 
 // LdsStack: the wavefront walks' stack.  The newest entries of a lane live
@@ -256,6 +257,13 @@ struct LdsStack {
     lds_uint2_t* t;            // next free slot: s + 64 * (sp - lo)
     uint2* g;                  // the lane's spill area (HBM)
     uint32_t sp, lo;           // entries; entries below lo are in HBM
+    static constexpr uint32_t kLaneBytes = 8u * kCap;   // LDS per lane
+    // windows: one 64-lane x kCap table per wave from `lds` on; `spill`: the lane's area
+    PTG_D void bind(void* lds, uint32_t wave, uint32_t lane, uint2* spill)
+    {
+        s = (lds_uint2_t*)(reinterpret_cast<uint2*>(lds) + wave * (64u * kCap) + lane);   // C cast: generic -> LDS
+        g = spill;
+    }
     PTG_D void reset()
     {
         sp = lo = 0;
@@ -298,6 +306,130 @@ struct LdsStack {
         const lds_u2v v = *t;
         return make_uint2(v.x, v.y);
     }
+    // whether n more entries fit the lane's spill area of `stride` entries (PTG_DEBUG)
+    PTG_D bool fits(uint32_t n, uint32_t stride) const { return sp + n <= stride; }
+};
+
+// The wavefront walks' stack: 4-byte slots (LdsSlotStack), or (word, near)
+// pairs (LdsStack, PTG_SLOT_STACK=0).  Window sizes in slots: 24 for the
+// closest-hit walk (a leaf takes two), 16 for the any-hit walk (one each).
+#ifndef PTG_SLOT_STACK
+#define PTG_SLOT_STACK 1
+#endif
+#ifndef PTG_STACK_SLOTS
+#define PTG_STACK_SLOTS 24
+#endif
+#ifndef PTG_STACK_SLOTS_ANY
+#define PTG_STACK_SLOTS_ANY 16
+#endif
+// LdsSlotStack: the same window in 4-byte slots (half the LDS per entry, so
+// more walk blocks fit a CU).  A block entry is one slot, its word: its near
+// need not be kept, because a block whose re-check at the pop would fail
+// holds only children that fail too (block_format.h, fact 1: their near is at
+// least the block's), so stepping it merely costs a block step.  A leaf entry
+// keeps its near - the leaf's own box test at its own time (fact 2) - in a
+// second slot under its word: NEAR = true (the closest-hit walk).  The
+// any-hit walk's tmax never shrinks, so every pushed entry passes its re-check
+// again at the pop (trace_shadow_ray: no ray_query_confirm): NEAR = false
+// keeps words only.  The word is always on top, so a pop reads the top two
+// slots with one ds_read2_b32 and takes the second only for a leaf.  Pushed
+// nears are positive floats (the clamped entry distance, node_block), so a
+// slot with the top bit set is always a leaf word, and a spill keeps leaf
+// entries whole by looking at the slot above its cut.
+template<bool NEAR>
+struct LdsSlotStack {
+    static constexpr uint32_t kCap = NEAR ? PTG_STACK_SLOTS : PTG_STACK_SLOTS_ANY;   // slots in the window
+    typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+    lds_u32_t* s;              // the lane's window column: slot k at s[64 * k]
+    lds_u32_t* t;              // next free slot: s + 64 * (sp - lo)
+    uint32_t* g;               // the lane's spill area (HBM), in slots
+    uint32_t sp, lo;           // slots; slots below lo are in HBM
+    static constexpr uint32_t kLaneBytes = 4u * kCap;   // LDS per lane
+    PTG_D void bind(void* lds, uint32_t wave, uint32_t lane, uint2* spill)
+    {
+        s = (lds_u32_t*)(reinterpret_cast<uint32_t*>(lds) + wave * (64u * kCap) + lane);   // C cast: generic -> LDS
+        g = reinterpret_cast<uint32_t*>(spill);
+    }
+    PTG_D void reset()
+    {
+        sp = lo = 0;
+        t = s;
+    }
+    PTG_D uint32_t size() const { return sp; }
+    // whether n more entries fit the lane's spill area of `stride` 8-byte
+    // entries, i.e. 2 * stride slots (PTG_DEBUG)
+    PTG_D bool fits(uint32_t n, uint32_t stride) const { return sp + (NEAR ? 2u : 1u) * n <= 2u * stride; }
+    // room for n more entries in the window (rare: spill the oldest half)
+    PTG_D void reserve(uint32_t n)
+    {
+        // put() writes two slots from the top whatever it keeps
+        if(sp - lo + (NEAR ? 2u * n : n) <= kCap) return;
+        const uint32_t in = sp - lo;
+        uint32_t h = in > 1 ? in / 2 : in;
+        if(NEAR && h < in && (s[64u * h] & kBeLeaf)) ++h;   // slot h - 1 is that leaf word's near: keep them together
+        for(uint32_t i = 0; i < h; ++i) g[lo + i] = s[64u * i];
+        for(uint32_t i = h; i < in; ++i) s[64u * (i - h)] = s[64u * i];
+        lo += h;
+        t = s + 64u * (sp - lo);
+    }
+    // write the entry at the top; keep it (push) iff `keep`
+    PTG_D void put(uint2 e, bool keep)
+    {
+        if(NEAR)
+        {
+            const bool leaf = (e.x & kBeLeaf) != 0;
+            t[0] = leaf ? e.y : e.x;
+            t[64] = e.x;
+            const uint32_t k = keep ? (leaf ? 2u : 1u) : 0u;
+            t += 64u * k;
+            sp += k;
+        }
+        else
+        {
+            t[0] = e.x;
+            if(keep)
+            {
+                t += 64;
+                ++sp;
+            }
+        }
+    }
+    // (word, near); a block's near reads as +0, which passes any tmax (tmax > 0)
+    PTG_D uint2 pop()
+    {
+        if(sp == lo)
+        {   // the window is empty: the entry comes back from HBM (rare)
+            const uint32_t w = g[sp - 1];
+            const bool leaf = NEAR && (w & kBeLeaf) != 0;
+            const uint32_t n = leaf ? g[sp - 2] : 0u;
+            sp -= leaf ? 2u : 1u;
+            lo = sp;
+            t = s;
+            return make_uint2(w, n);
+        }
+        if(!NEAR)
+        {
+            --sp;
+            t -= 64;
+            return make_uint2(*t, 0u);
+        }
+        // one ds_read2_b32 (the slot under the window's bottom, read for a
+        // block, is LDS of this block and unused)
+        const uint32_t w = t[-64], n = t[-128];
+        const bool leaf = (w & kBeLeaf) != 0;
+        const uint32_t k = leaf ? 2u : 1u;
+        t -= 64u * k;
+        sp -= k;
+        return make_uint2(w, leaf ? n : 0u);
+    }
+};
+
+template<bool ANY> struct WalkStackOf {
+#if PTG_SLOT_STACK
+    typedef LdsSlotStack<!ANY> type;
+#else
+    typedef LdsStack type;
+#endif
 };
 
 // x_t for t in 0..3, as two selects on t's bits: by value, so that the
@@ -611,9 +743,20 @@ struct BlockWalker {
         else
         {   // a lane with a zero or denormal direction component: the
             // reference's min/max form (an unordered pair gives the same);
-            // an infinite reciprocal can pass an unused slot's infinite planes
+            // an infinite reciprocal can pass an unused slot's infinite planes.
+            // The entry distance is clamped as in the other form: max(near,
+            // tmin_p) < tmax <=> near < tmax whenever tmin_p < tmax, and a
+            // walk's tmax is never below tmin_p (the initial tmax, or a
+            // confirmed t > tmin); at tmax == tmin_p no triangle can be
+            // accepted any more.  A pushed near is then a positive float
+            // (LdsSlotStack tells its slots from leaf words by the top bit).
+            const float tmin_p = __uint_as_float(__float_as_uint(tmin) + 1u);
 #pragma unroll
-            for(uint32_t j = 0; j < W; ++j) hits |= (box(l[j], h[j], nr[j]) && !(a[j] & kBeNone)) ? (1u << j) : 0u;
+            for(uint32_t j = 0; j < W; ++j)
+            {
+                hits |= (box(l[j], h[j], nr[j]) && !(a[j] & kBeNone)) ? (1u << j) : 0u;
+                nr[j] = fmaxf(nr[j], tmin_p);
+            }
         }
         if(COUNT)
         {
@@ -650,7 +793,7 @@ struct BlockWalker {
         if(rest)
         {   // written at the top either way, kept only if pushed
             // (the host's stack bound, which sizes the spill areas, must hold)
-            PTG_CHECK(sc, st.size() + uint32_t(__builtin_popcount(rest)) <= sc.spill_stride, kDebugStack);
+            PTG_CHECK(sc, st.fits(uint32_t(__builtin_popcount(rest)), sc.spill_stride), kDebugStack);
             st.reserve(W - 1);
 #pragma unroll
             for(uint32_t j = W - 1; j >= 1; --j) st.put(make_uint2(a[j], __float_as_uint(nr[j])), (rest >> j) & 1u);

@@ -97,8 +97,21 @@ template<typename T> PTG_D void st_state(T* p, T value)
 template<typename T> PTG_D T ld_out(const T* p) { return ld_state(p); }
 template<typename T> PTG_D void st_out(T* p, T value) { st_state(p, value); }
 
+#ifndef PTG_PACK_BATT
+#define PTG_PACK_BATT 0
+#endif
+// PTG_PACK_BATT: the bounce's bsdf attenuation rides in the spare w words of
+// meta, ray_o and ray_d (16 B less path state per path read and written)
 PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
 {
+#if PTG_PACK_BATT
+    st_state(S.meta + q, make_uint4(p.meta.x, p.meta.y, p.meta.z, __float_as_uint(p.batt.x)));
+    st_state(S.seed + q, p.seed);
+    st_state(S.ray_o + q, make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, p.batt.y));
+    st_state(S.ray_d + q, make_float4(p.ray_d.x, p.ray_d.y, p.ray_d.z, p.batt.z));
+    st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
+    st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
+#else
     st_state(S.meta + q, p.meta);
     st_state(S.seed + q, p.seed);
     st_state(S.ray_o + q, make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, 0.f));
@@ -106,6 +119,7 @@ PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
     st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
     st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
     st_state(S.batt + q, make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f));
+#endif
     if(!meta_nee(p.meta)) return;   // no pending NEE ray: its records are never read
     st_state(S.nee_c + q, make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf));
     st_state(S.nee_d + q, make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter));
@@ -120,8 +134,9 @@ PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
     PathRec p;
     p.meta = ld_state(S.meta + q);
     p.seed = ld_state(S.seed + q);
-    p.ray_o = xyz(ld_state(S.ray_o + q));
-    p.ray_d = xyz(ld_state(S.ray_d + q));
+    const float4 ro = ld_state(S.ray_o + q), rd = ld_state(S.ray_d + q);
+    p.ray_o = xyz(ro);
+    p.ray_d = xyz(rd);
     if(!carried)
     {
         p.att = p.contrib = p.batt = V3(0, 0, 0);
@@ -142,7 +157,11 @@ PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
     p.reg = a.w;
     p.contrib = xyz(c);
     p.bpdf = c.w;
+#if PTG_PACK_BATT
+    p.batt = V3(__uint_as_float(p.meta.w), ro.w, rd.w);
+#else
     p.batt = xyz(ld_state(S.batt + q));
+#endif
     p.nee.color = xyz(nc);
     p.nee.mis_pdf = nc.w;
     p.nee.dir = xyz(nd);

@@ -19,6 +19,9 @@
 #include <cfloat>
 
 namespace ptg {
+#ifdef PTG_MODEL_HOOKS
+float g_model_blas_traversal_cost = 2.0f;
+#endif
 namespace {
 
 using namespace hm;
@@ -32,6 +35,7 @@ struct TreeNode {
 };
 
 struct Builder {
+    float traversal_cost = 2.0f;     // bvh.cc:111-112
     std::vector<TreeNode> pool;
     std::vector<f3> pre_min, pre_max, suf_min, suf_max;
 
@@ -91,7 +95,7 @@ struct Builder {
         }
         f3 size = pool[self].max - pool[self].min;
         best /= half_area(size);
-        best += 2.0f;
+        best += traversal_cost;
         const bool keep_leaves = float(n) <= best;
         if(keep_leaves)
         {
@@ -150,9 +154,10 @@ struct Builder {
 
 } // namespace
 
-ptg_bvh build_bvh(std::vector<BuildLeaf>& leaves, BvhBuffers& bc)
+ptg_bvh build_bvh(std::vector<BuildLeaf>& leaves, BvhBuffers& bc, float traversal_cost)
 {
     Builder b;
+    b.traversal_cost = traversal_cost;
     b.pool.reserve(leaves.size() * 2 + 1);
     TreeNode root;
     root.min = v3(FLT_MAX, FLT_MAX, FLT_MAX);
@@ -204,7 +209,13 @@ ptg_bvh build_blas(const ptg_mesh& m, const MeshBuffers& mb, BvhBuffers& out)
         f3 p2 = mb.pos[m.base_vertex_offset + tri[2]];
         leaves.push_back(BuildLeaf{vmin(p0, vmin(p1, p2)), vmax(p0, vmax(p1, p2)), i});
     }
+#ifdef PTG_MODEL_HOOKS
+    // tools/walk_sim ANYHIER (model builds only): BLASes with another SAH
+    // traversal cost, the same leaves and leaf boxes
+    return build_bvh(leaves, out, g_model_blas_traversal_cost);
+#else
     return build_bvh(leaves, out);
+#endif
 }
 
 ptg_bvh build_tlas(size_t count, const ptg_tlas_instance* const* instances, const uint32_t* ids,

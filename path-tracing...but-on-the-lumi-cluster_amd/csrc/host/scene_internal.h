@@ -33,7 +33,10 @@ struct BuildLeaf {
 };
 
 // build_generic_bvh (bvh.cc:195-229): appends nodes + 8 link orders.
-ptg_bvh build_bvh(std::vector<BuildLeaf>& leaves, BvhBuffers& out);
+ptg_bvh build_bvh(std::vector<BuildLeaf>& leaves, BvhBuffers& out, float traversal_cost = 2.0f);
+#ifdef PTG_MODEL_HOOKS
+extern float g_model_blas_traversal_cost;   // tools/walk_sim ANYHIER: the BLAS builds' SAH traversal cost
+#endif
 // build_blas (bvh.cc:231-250)
 ptg_bvh build_blas(const ptg_mesh& m, const MeshBuffers& mb, BvhBuffers& out);
 // build_tlas (bvh.cc:252-284): instances[i] with leaf payload ids[i]

@@ -233,8 +233,13 @@ constexpr int kRefillIdle = 24;   // refill once at least this many lanes are id
 #define PTG_SHADOW_WAVES 6
 #define PTG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(ANY ? PTG_SHADOW_WAVES : PTG_WALK_WAVES, 8)))
 constexpr int kWalkUnroll = 2;     // node steps per leaf phase (1 and 3 measured slower)
-constexpr uint32_t kWalkResident = 4;      // walk blocks the LDS holds per CU (16-entry stack windows: 4 x 40 KB)
-constexpr uint32_t kWalkBlocksPerCu = 3;   // walk grid: blocks per CU (one resident wave, see ptg_context_create)
+// Walk residency per walk kind (closest hit, any hit): the LDS of a walk
+// block is padded to 1 / kWalkResident of the CU's (0: not padded), and the
+// grid holds kWalkBlocksPerCu blocks per CU (one resident wave, see
+// ptg_context_create).  Timing knobs PTG_WALK_RESIDENT[_ANY] and
+// PTG_WALK_BLOCKS[_ANY] override them (the results do not depend on them).
+constexpr uint32_t kWalkResident[2] = {4, 4};
+constexpr uint32_t kWalkBlocksPerCu[2] = {3, 3};
 constexpr uint32_t kWfSlots = 2;           // concurrent wavefront chunk pipelines (ptg_context::Slot)
 constexpr uint32_t kBands = 1024;   // XCD bands of a walk queue: a multiple of the XCD count (8 on MI355X)
 // a chunk's device counters: per round the queue / NEE list lengths (2 words,
@@ -284,8 +289,13 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     // then usually the same pixels' next 8 samples (or the next pixels), so
     // the occluder its last group found (the candidate, try_candidate) lies on
     // the new rays' way to the sun too.  The closest-hit walk keeps runs of 1.
-    constexpr uint32_t R = ANY ? kAnyRun : 1u;
-    const uint32_t runs = (local + R - 1u) / R;
+    // Runs only where they keep a run inside one band and still leave every
+    // wave work (small queues - late rounds, small frames, tile renders - take
+    // single groups: a run crossing bands would jump nxcd * band groups).
+    static_assert((kAnyRun & (kAnyRun - 1u)) == 0, "kAnyRun is a power of two");
+    const uint32_t rl = (ANY && band >= kAnyRun && groups >= waves * kAnyRun) ? uint32_t(__builtin_ctz(kAnyRun)) : 0u;
+    const uint32_t R = 1u << rl;
+    const uint32_t runs = (local + R - 1u) >> rl;
     const uint32_t end = wave < runs ? ((runs - wave + waves - 1) / waves) * R * 64u : 0u;
     uint32_t cursor = 0;
     const float tmin = (ANY || round > 0) ? MIN_RAY_DIST : 0.0f;
@@ -294,10 +304,9 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     // LDS: every lane's world ray, then the stack windows, one 64-lane x kCap
     // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
-    BlockWalker<LdsCold, LdsStack> w;
-    w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C casts: generic -> LDS address space
-    w.st.s = (lds_uint2_t*)(reinterpret_cast<uint2*>(cold + blockDim.x) + (threadIdx.x >> 6) * (64u * LdsStack::kCap) + lane);
-    w.st.g = sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride;
+    BlockWalker<LdsCold, typename WalkStackOf<ANY>::type> w;
+    w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C cast: generic -> LDS address space
+    w.st.bind(cold + blockDim.x, threadIdx.x >> 6, lane, sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride);
     bool active = false;
     uint32_t q = 0;
     // ANY: the wave's latest occluder (instance, triangle), wave-uniform (in
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
                 {
                     const uint32_t v = cursor + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
                     const uint32_t k = v >> 6;   // this wave's k-th group
-                    const uint32_t l = (wave + (k / R) * waves) * R + k % R;
+                    const uint32_t l = (wave + (k >> rl) * waves) * R + (k & (R - 1u));
                     const uint32_t t = ((xcd + nxcd * (l / band)) * band + l % band) * 64u + (v & 63u);
                     if(v < end && l < local && t < n)
                     {
@@ -1368,6 +1377,17 @@ int timed_end(ptg_context* ctx, hipStream_t st)
 
 extern "C" {
 
+// a launch-geometry knob from the environment (timing experiments only:
+// no result depends on it), else its default
+static uint32_t env_knob(const char* name, uint32_t dflt)
+{
+    const char* v = getenv(name);
+    if(!v || !*v) return dflt;
+    char* end = nullptr;
+    const unsigned long x = strtoul(v, &end, 10);
+    return (end && *end == 0 && x <= 64) ? uint32_t(x) : dflt;
+}
+
 int ptg_context_create(int device, ptg_context** out)
 {
     if(!out) return fail(PTG_E_INVALID, "null out");
@@ -1389,9 +1409,13 @@ int ptg_context_create(int device, ptg_context** out)
     // window (8 x kCap B) in LDS, so the walk blocks' LDS sets how many are
     // resident per CU: kWalkResident (the LDS is padded to that share).
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
-    const uint32_t lds_need = kBlock * uint32_t(sizeof(WalkCold) + sizeof(uint2) * LdsStack::kCap);
+    const uint32_t lds_need[2] = {kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<false>::type::kLaneBytes),
+                                  kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<true>::type::kLaneBytes)};
     for(int k = 0; k < 2; ++k)
-        ctx->walk_lds[k] = std::max<uint32_t>(lds_need, (lds_cu / kWalkResident) / 1024u * 1024u);
+    {
+        const uint32_t resident = env_knob(k ? "PTG_WALK_RESIDENT_ANY" : "PTG_WALK_RESIDENT", kWalkResident[k]);
+        ctx->walk_lds[k] = std::max<uint32_t>(lds_need[k], resident ? (lds_cu / resident) / 1024u * 1024u : 0u);
+    }
     // One wave of walk blocks, 3 per CU although the LDS holds 4: every block
     // is resident from the start (no oversubscription), and the fourth slot's
     // LDS and registers take the other chunk pipeline's shade and sky waves,
@@ -1407,8 +1431,9 @@ int ptg_context_create(int device, ptg_context** out)
         per_cu = 0;
         if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walks[k], kBlock, ctx->walk_lds[k]) != hipSuccess ||
            per_cu <= 0)
-            per_cu = int(kWalkResident);
-        ctx->walk_grid[k] = std::min<uint32_t>(uint32_t(per_cu), kWalkBlocksPerCu) * uint32_t(prop.multiProcessorCount);
+            per_cu = int(kWalkResident[k] ? kWalkResident[k] : 1u);
+        const uint32_t blocks = env_knob(k ? "PTG_WALK_BLOCKS_ANY" : "PTG_WALK_BLOCKS", kWalkBlocksPerCu[k]);
+        ctx->walk_grid[k] = std::min<uint32_t>(uint32_t(per_cu), std::max(1u, blocks)) * uint32_t(prop.multiProcessorCount);
         ctx->walk_xcds[k] = (ctx->walk_grid[k] % 8 == 0 && kBands % 8 == 0) ? 8u : 1u;
     }
     PTG_HIP(hipSetDevice(device));
@@ -1589,7 +1614,10 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     };
     std::vector<InstBox> ib(instance_count);
     {
-        std::vector<uint32_t> seen(instance_count, 0);
+        // seen: the distinct subframes whose TLAS names the instance; an
+        // instance named twice by one TLAS is never a candidate (the
+        // reference builder makes no such frame, the public upload could)
+        std::vector<uint32_t> seen(instance_count, 0), last_sf(instance_count, 0xFFFFFFFFu);
         for(size_t i = 0; i < instance_count; ++i)
         {
             const uint32_t tris = leaf_bounds_ok(instances[i]) ? instances[i].m.triangle_count : 0u;
@@ -1607,12 +1635,21 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
                 if(i >= instance_count) continue;
                 const ptg_bvh_node& nd = frame_nodes[base + n];
                 const InstBox b{{nd.min_x, nd.min_y, nd.min_z}, uint32_t(sf), {nd.max_x, nd.max_y, nd.max_z}, ib[i].tri_count};
+                if(last_sf[i] == uint32_t(sf))
+                {   // twice in this subframe's TLAS
+                    ib[i].sub = kInstNoCandidate;
+                    seen[i] = 0xFFFFFFFFu;
+                    continue;
+                }
+                last_sf[i] = uint32_t(sf);
+                if(seen[i] == 0xFFFFFFFFu) continue;
                 if(seen[i]++ == 0) ib[i] = b;
                 else if(memcmp(ib[i].lo, b.lo, 12) != 0 || memcmp(ib[i].hi, b.hi, 12) != 0) ib[i].sub = kInstNoCandidate;
             }
         }
         for(size_t i = 0; i < instance_count; ++i)
-            if(seen[i] > 1 && ib[i].sub != kInstNoCandidate)
+            if(seen[i] == 0xFFFFFFFFu) ib[i].sub = kInstNoCandidate;
+            else if(seen[i] > 1 && ib[i].sub != kInstNoCandidate)
                 ib[i].sub = seen[i] == subframe_count ? kInstAllSubframes : kInstNoCandidate;
     }
 
@@ -1854,6 +1891,16 @@ int ptg_trace_rays(ptg_context* ctx, uint32_t subframe, size_t n, const float* r
     if(subframe >= ctx->subframe_count) return fail(PTG_E_RANGE, "subframe out of range");
     if(!n) return PTG_OK;
     if(!rays || !hits || n >= (1u << 28)) return fail(PTG_E_INVALID, "ptg_trace_rays: bad arguments");
+    // the walk's one-compare box test takes the float after tmin by +1 on its
+    // bits (BlockWalker::node_block), which needs tmin's sign bit clear; the
+    // reference's queries use 0 and MIN_RAY_DIST (path_tracer.hh:342, :420)
+    for(size_t i = 0; i < n; ++i)
+    {
+        uint32_t b;
+        memcpy(&b, rays + i * 8 + 6, 4);
+        if((b & 0x80000000u) && (b & 0x7FFFFFFFu) <= 0x7F800000u)
+            return fail(PTG_E_INVALID, "ptg_trace_rays: ray " + std::to_string(i) + " has a negative or -0 tmin (needs tmin >= +0)");
+    }
     PTG_HIP(ctx->grow(ctx->tmp_a, n * 32));
     PTG_HIP(ctx->grow(ctx->tmp_b, n * 32));
     PTG_HIP(hipMemcpyAsync(ctx->tmp_a.p, rays, n * 32, hipMemcpyHostToDevice, ctx->stream));

@@ -103,6 +103,63 @@ def assemble_numpy(shard: TileShard, gathered, image):
     return image
 
 
+class ShardMismatch(RuntimeError):
+    """The ranks of one collective render disagree on its shape (raised on every rank)."""
+
+
+_FIELDS = ("kind", "width", "height", "spp", "bounces", "student_id", "blur_step", "a", "b", "world", "rank", "group_ok")
+
+
+def _agree(kind, cfg, a, b, shard_rank, shard_world, group_ok, dev, what):
+    """Before any rank renders or enters the data collective, every rank of
+    the default group all-gathers one small record of the call: the kind of
+    shard, the config (config.hh's macros), the shard's two size parameters
+    (tile size, or image size), its world size and rank, and whether it
+    describes this process's place in the group.  Every rank then checks every
+    record and raises ShardMismatch on any disagreement, so a rank with
+    another tile size, SPP or world size makes ALL ranks fail within one
+    small collective, instead of the others waiting in a gather of different
+    buffer sizes until the group's timeout (status, no
+    hang).  On RCCL the record is a device tensor on the current stream; the
+    host reads it back (one small synchronisation per call)."""
+    import torch
+    import torch.distributed as dist
+    mine = [kind, int(cfg.width), int(cfg.height), int(cfg.samples_per_pixel), int(cfg.max_bounces),
+            int(cfg.student_id), int(cfg.samples_per_motion_blur_step), int(a), int(b), int(shard_world),
+            int(shard_rank), 1 if group_ok else 0]
+    on = dev if (dist.get_backend() != "gloo" and dev.type == "cuda") else torch.device("cpu")
+    t = torch.tensor(mine, dtype=torch.int64, device=on)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    recs = torch.stack(parts).cpu().tolist()
+    bad = [r for r, rec in enumerate(recs) if not rec[11]]
+    if bad:
+        raise ShardMismatch("%s: rank(s) %s hold a shard that is not their place in the process group (%s)"
+                            % (what, bad, ", ".join("rank %d: shard %d of %d" % (r, recs[r][10], recs[r][9]) for r in bad)))
+    keys = [tuple(rec[:10]) for rec in recs]
+    if any(k != keys[0] for k in keys):
+        names = list(_FIELDS)
+        names[7:9] = ("tile_w", "tile_h") if kind == 1 else ("image_h", "image_w")
+        diff = [i for i in range(10) if len({k[i] for k in keys}) > 1]
+        raise ShardMismatch("%s: the ranks disagree on %s (%s)" % (what, ", ".join(names[i] for i in diff), "; ".join(
+            "rank %d: %s" % (r, {names[i]: rec[i] for i in diff}) for r, rec in enumerate(recs))))
+    return recs
+
+
+def _collective_mode(shard, force_collective, what):
+    """Whether the call runs collectives: a shard of more than one rank needs
+    the default process group (and then every rank agrees on the call first,
+    _agree); a one-rank shard is rendered locally, unless it is the whole
+    group of one and `force_collective` asks for the collective anyway."""
+    import torch.distributed as dist
+    grouped = dist.is_available() and dist.is_initialized()
+    if shard.world == 1:
+        return bool(grouped and dist.get_world_size() == 1 and force_collective)
+    if not grouped:
+        raise RuntimeError("%s: world size %d but no process group" % (what, shard.world))
+    return True
+
+
 def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force_collective=True):
     """Render this rank's tiles and gather them into `image` on rank 0.
 
@@ -113,16 +170,14 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
     RCCL then orders the collective after the tiles were written, and the
     scatter after the collective, with no host synchronisation.
 
-    The collective runs when the shard describes this process's place in the
-    default process group (shard.world == group size, shard.rank == group
-    rank; at world size 1 too, with `force_collective`).  A one-rank shard
-    (shard.world == 1) in a larger job, or with no group, is rendered locally.
-    Any other mismatch raises on the rank that has it, before that rank
-    renders.  The check is local: a rank whose own shard matches still enters
-    the gather, which then fails only when the mismatched rank's process exits
-    (or at the group's timeout).  Build every rank's shard from the same
-    (cfg, tile size, world size).  Over gloo (CPU groups: tests, rehearsals)
-    the tiles go through host memory.
+    A shard of more than one rank runs the collectives of the default process
+    group (and a one-rank shard at world size 1 too, with `force_collective`);
+    a one-rank shard in a larger job, or with no group, is rendered locally.
+    Before anything is rendered the ranks agree on the call (_agree): if any
+    rank's config, tile size or world size differs, or its shard is not its
+    place in the group, EVERY rank raises ShardMismatch (no rank waits in a
+    gather of other sizes).  Over gloo (CPU groups: tests, rehearsals) the
+    tiles go through host memory.
     """
     import contextlib
 
@@ -130,18 +185,12 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
     import torch.distributed as dist
     dev = image.device
     per_tile = shard.tile_w * shard.tile_h
-    grouped = dist.is_available() and dist.is_initialized()
-    if grouped and dist.get_world_size() == shard.world and dist.get_rank() == shard.rank:
-        collective = shard.world > 1 or force_collective
-    elif shard.world == 1:
-        collective = False
-    elif not grouped:
-        raise RuntimeError("render_and_gather: world size %d but no process group" % shard.world)
-    else:
-        raise RuntimeError("render_and_gather: shard (rank %d of %d) does not match the process group (rank %d of %d)"
-                           % (shard.rank, shard.world, dist.get_rank(), dist.get_world_size()))
+    collective = _collective_mode(shard, force_collective, "render_and_gather")
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
     with ctx:
+        if collective:
+            _agree(1, cfg, shard.tile_w, shard.tile_h, shard.rank, shard.world,
+                   dist.get_world_size() == shard.world and dist.get_rank() == shard.rank, dev, "render_and_gather")
         buf = torch.zeros((shard.max_count * per_tile, 4), dtype=torch.uint8, device=dev)
         if shard.count:
             renderer.render_tiles(cfg, shard.tile_w, shard.tile_h, shard.first, shard.stride, shard.count,
@@ -201,29 +250,25 @@ def render_and_reduce(renderer, cfg, shard: SampleShard, image, accum=None, stre
     sum of the partials, so the frame is within float32 rounding of the
     single-GPU render, not bit-identical to it (module docstring).
 
-    Like render_and_gather: everything is issued on `stream`, the collective
-    runs when the shard describes this process's place in the default group
-    (at world size 1 too, with `force_collective`), and a mismatch raises on
-    the rank that has it.  RCCL reduces the device tensors over xGMI; gloo
+    Like render_and_gather: everything is issued on `stream`, which must be
+    the stream the renderer launches on (GpuRenderer.set_stream(stream)), so
+    that RCCL orders the reduce after the partial was written and
+    tonemap_device after the reduce; the ranks agree on the call first
+    (config, image size, world size and place in the group: any disagreement
+    raises ShardMismatch on every rank before anything is rendered).  RCCL reduces the device tensors over xGMI; gloo
     (CPU groups: tests, rehearsals) reduces through host memory."""
     import contextlib
 
     import torch
     import torch.distributed as dist
     dev = image.device
-    grouped = dist.is_available() and dist.is_initialized()
-    if grouped and dist.get_world_size() == shard.world and dist.get_rank() == shard.rank:
-        collective = shard.world > 1 or force_collective
-    elif shard.world == 1:
-        collective = False
-    elif not grouped:
-        raise RuntimeError("render_and_reduce: world size %d but no process group" % shard.world)
-    else:
-        raise RuntimeError("render_and_reduce: shard (rank %d of %d) does not match the process group (rank %d of %d)"
-                           % (shard.rank, shard.world, dist.get_rank(), dist.get_world_size()))
+    collective = _collective_mode(shard, force_collective, "render_and_reduce")
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
     with ctx:
         h, w = image.shape[0], image.shape[1]
+        if collective:
+            _agree(2, cfg, h, w, shard.rank, shard.world,
+                   dist.get_world_size() == shard.world and dist.get_rank() == shard.rank, dev, "render_and_reduce")
         part = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
         if shard.j1 > shard.j0:
             renderer.render(cfg, samples=(shard.j0, shard.j1), out_accum=part)

@@ -22,6 +22,15 @@ GPU-vs-shipped numbers.  Both builds are the reference's own sources
 
 Usage: python tests/golden/parity_stats.py [--frames 0 450] [--rows y0 y1]
 writes tests/golden/parity_stats.json (whole frames by default).
+
+  --metric [--spp N]   the same tiers at the metric configuration's image
+      (1280x720, N spp, default 256): T2 / T3 over the
+      whole frames (the reference's `render`: baseline_render's semantics),
+      T1 over the 16-row band 352-368 (per-sample radiances of both builds),
+      plus T3v, validator.py's own acceptance figure (validator.py:43-54:
+      each image downscaled 2x by the 2x2 mean + truncation, the shipped
+      build's as the reference frame); merged into parity_stats.json under
+      "metric_config".
 """
 import argparse
 import json
@@ -87,13 +96,65 @@ def frame_stats(assets, frame, y0, y1):
     }
 
 
+def metric_stats(assets, frame, w, h, spp, band=(352, 368)):
+    """T1 on a band, T2 / T3 / T3v on the whole frame, strict vs shipped, at w x h x spp."""
+    from oracle import Reference
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "ptv", os.path.join(ROOT, "path-tracing...but-on-the-lumi-cluster_amd", "validator.py"))
+    V = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(V)
+    refs = {m: Reference(m, w, h, spp, BOUNCES) for m in ("strict", "v3")}
+    for r in refs.values():
+        if not r.available():
+            raise FileNotFoundError(r.exe)
+    acc, bgra = {}, {}
+    for m, r in refs.items():
+        acc[m], bgra[m] = r.render(assets, frame)
+    y0, y1 = band
+    smp = {m: r.samples(assets, frame, 0, y0, w, y1 - y0, 0, spp)[..., :3] for m, r in refs.items()}
+    t1 = within(smp["strict"], smp["v3"]).all(-1)
+    a_s, a_v = acc["strict"][..., :3], acc["v3"][..., :3]
+    t2 = within(a_s, a_v).all(-1)
+    mean_s = a_s.reshape(-1, 3).mean(0, dtype=np.float64)
+    mean_v = a_v.reshape(-1, 3).mean(0, dtype=np.float64)
+    rel = np.abs(a_s - a_v) / np.maximum(np.maximum(np.abs(a_s), np.abs(a_v)), 1e-30)
+    worst = rel.max(-1)
+    b_s, b_v = bgra["strict"], bgra["v3"]
+    ref_half = V.downscale_half(V.bgra_to_rgb(b_v))          # the shipped build's frame as validator.py's reference
+    p_val, good = V.validate_frame(ref_half, b_s)
+    return {
+        "frame": frame, "band_rows": [y0, y1], "samples_in_band": int(t1.size), "pixels": int(t2.size),
+        "T1_samples_within_1e-4": round(float(t1.mean()), 5),
+        "T2_pixels_within_1e-4": round(float(t2.mean()), 5),
+        "T2_pixels_within_1e-3": round(float((worst <= 1e-3).mean()), 5),
+        "T2_pixels_within_1e-2": round(float((worst <= 1e-2).mean()), 5),
+        "T2_median_rel_diff": float("%.3g" % np.median(worst)),
+        "T2_image_mean_rel_diff": [round(float(x), 7) for x in np.abs(mean_v - mean_s) / np.abs(mean_s)],
+        "T3_psnr_db": round(psnr(b_s[..., :3], b_v[..., :3]), 3),
+        "T3_pixels_byte_exact": round(float((b_s == b_v).all(-1).mean()), 5),
+        "T3v_validator_psnr_db": round(float(p_val), 3), "T3v_validator_good": bool(good),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--metric", action="store_true")
+    ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--frames", type=int, nargs="*", default=[0, 450])
     ap.add_argument("--rows", type=int, nargs=2, default=[0, H])
     ap.add_argument("--out", default=os.path.join(HERE, "parity_stats.json"))
     a = ap.parse_args()
     assets = os.path.join(ROOT, "assets")
+    if a.metric:
+        w, h = 1280, 720
+        res = json.load(open(a.out)) if os.path.exists(a.out) else {}
+        res["metric_config"] = {"width": w, "height": h, "spp": a.spp, "bounces": BOUNCES,
+                                "frames": [metric_stats(assets, f, w, h, a.spp) for f in a.frames]}
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res["metric_config"], indent=1))
+        return
     res = {"config": {"width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
                       "builds": {"strict": "-O2 -ffp-contract=off -fno-fast-math (== the GPU path, bit for bit)",
                                  "v3": "-O3 -ffast-math -march=x86-64-v3 (the reference Makefile's flags, "

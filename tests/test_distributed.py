@@ -132,7 +132,7 @@ def _mismatch_worker(rank, world, port, out):
         D.render_and_gather(StubRenderer(rank), cfg, D.TileShard(cfg, 16, 8, rank, world + 1), image)
         refused = False
     except RuntimeError as e:
-        refused = "does not match the process group" in str(e)
+        refused = isinstance(e, D.ShardMismatch) and "not their place in the process group" in str(e)
     np.save(out % rank, np.array([ok, refused]))
     dist.barrier()
     dist.destroy_process_group()
@@ -231,3 +231,51 @@ def test_reduce_assembles_radiance_gloo(tmp_path, world):
     want /= spp
     assert np.allclose(acc[..., 0], want, rtol=1e-5, atol=1e-7)
     assert np.allclose(acc[..., 2], 3 * want, rtol=1e-5, atol=1e-7)
+
+
+# ---- ranks that disagree on the call fail together ------
+
+def _disagree_worker(rank, world, port, case, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
+    t0 = time.monotonic()
+    msg, rendered = "", False
+    try:
+        if case == "tile":        # only rank 1 cuts other tiles
+            cfg = N.RenderConfig.make(40, 20, 8)
+            stub = StubRenderer(rank)
+            D.render_and_gather(stub, cfg, D.TileShard(cfg, 16 if rank == 0 else 8, 8, rank, world),
+                                torch.zeros((20, 40, 4), dtype=torch.uint8))
+            rendered = bool(stub.calls)
+        elif case == "spp":       # only rank 1 renders another SPP
+            cfg = N.RenderConfig.make(30, 20, 48 if rank == 0 else 56)
+            stub = StubSampleRenderer()
+            D.render_and_reduce(stub, cfg, D.SampleShard(cfg, rank, world), torch.zeros((20, 30, 4), dtype=torch.uint8))
+            rendered = bool(stub.calls)
+        elif case == "world":     # only rank 1's shard is not its place in the group
+            cfg = N.RenderConfig.make(40, 20, 8)
+            stub = StubRenderer(rank)
+            D.render_and_gather(stub, cfg, D.TileShard(cfg, 16, 8, rank, world if rank == 0 else world + 1),
+                                torch.zeros((20, 40, 4), dtype=torch.uint8))
+            rendered = bool(stub.calls)
+    except D.ShardMismatch as e:
+        msg = str(e)
+    np.save(out % rank, np.array([msg, str(rendered), str(time.monotonic() - t0)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,field", [("tile", "disagree on tile_w"), ("spp", "disagree on spp"), ("world", "not their place")])
+def test_disagreeing_rank_fails_every_rank(tmp_path, case, field):
+    """render_and_gather / render_and_reduce: when ONE rank's call differs
+    (tile size, SPP, or a shard that is not its place in the group), every
+    rank raises ShardMismatch within seconds and nothing is rendered - the
+    others do not wait in a gather or reduce of other buffer sizes."""
+    out = str(tmp_path / "r%d.npy")
+    mp.spawn(_disagree_worker, args=(2, _free_port(), case, out), nprocs=2, join=True)
+    for r in range(2):
+        msg, rendered, secs = np.load(out % r).tolist()
+        assert field in msg, (r, msg)
+        assert rendered == "False"
+        assert float(secs) < 30

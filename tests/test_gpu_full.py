@@ -99,6 +99,13 @@ def test_errors_not_faults(gpu, assets_dir):
         gpu.render(cfg, samples=(0, 40))                        # 5 subframes needed, the frame has 4
     with pytest.raises(N.PtgError, match=r"\(-6\)"):
         gpu.trace_rays(9, np.zeros((4, 8), np.float32))
+    # a negative or -0 tmin is outside ptg_trace_rays' contract (ptg.h): refused, not traced
+    for tmin in (-1.0, -0.0):
+        rays = np.zeros((4, 8), np.float32)
+        rays[:, 5], rays[:, 7] = 1.0, 1e9
+        rays[2, 6] = tmin
+        with pytest.raises(N.PtgError, match=r"\(-1\).*ray 2 .*tmin"):
+            gpu.trace_rays(0, rays)
     with pytest.raises(N.PtgError, match=r"\(-6\)"):
         gpu.path_trace_samples(cfg, np.array([[640, 0]]), np.array([0]))
     with pytest.raises(N.PtgError, match=r"\(-6\)"):

@@ -20,7 +20,7 @@ open(os.path.join(sys.argv[1], ".rebuild_host"), "w").write(rev + "\n")
 # entry points the current C ABI declares but the old sources lack: stubs (timing builds only)
 p = os.path.join(sys.argv[1], "pt_kernels.hip")
 s = open(p).read()
-stubs = {"ptg_arith_selftest": 'extern "C" int ptg_arith_selftest(ptg_context*) { return 0; }',
+stubs = {"ptg_arith_selftest": 'extern "C" int ptg_arith_selftest(ptg_context*) { return -1; }   /* not available: never a passing self-test */',
          "ptg_tonemap_device": 'extern "C" int ptg_tonemap_device(ptg_context*, size_t, const ptg_float4*, ptg_uchar4*) { return -1; }'}
 for name, body in stubs.items():
     if name not in s:

@@ -18,11 +18,18 @@
 //   CLOSEBOUND=1  closest-hit walks started with tmax just above their own hit
 //   OCC=1, ANYORDER, CLOSEORDER, ORDERLEVEL, LOCKSTEP, CACHESIM, PACKET, SPEC,
 //   NONEAR, SCHED   (see their blocks below)
+//   ANYHIER=c     (walk_simh build) any-hit walks also over BLASes rebuilt with
+//                 SAH traversal cost c (the same triangle leaves and leaf boxes;
+//                 the any-hit result is the OR over leaves, so only the leaf
+//                 boxes must be the reference's): same results, step counts
 // It also prints the share of the mix's shadow rays whose sun ray is blocked
 // by the ground (the surface pass leaves those untraced, nee_shadow_moot).
 #include "ptg.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/block_bvh.h"
 #include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/hmath.h"
+#ifdef PTG_MODEL_HOOKS
+#include "../path-tracing...but-on-the-lumi-cluster_amd/csrc/host/scene_internal.h"
+#endif
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -954,6 +961,44 @@ int main(int argc, char** argv)
         return wrong ? 1 : 0;
     }
 
+    // ANYHIER: a second scene whose BLASes are rebuilt with another SAH
+    // traversal cost (tools/Makefile walk_simh); its instances, meshes and
+    // TLAS leaves must be the first scene's
+    ptg_scene* sceneB = nullptr;
+    ptg_scene_view vB{};
+    Packed pkB;
+    if(const char* hc = getenv("ANYHIER"))
+    {
+#ifdef PTG_MODEL_HOOKS
+        g_model_blas_traversal_cost = float(atof(hc));
+        const int e1 = ptg_scene_load(argv[1], &cfg, &sceneB);
+        g_model_blas_traversal_cost = 2.0f;
+        if(e1 || ptg_scene_setup_frame(sceneB, frame)) { fprintf(stderr, "ANYHIER scene: %s\n", ptg_last_error()); return 1; }
+        ptg_scene_view_get(sceneB, &vB);
+        size_t diff = vB.instance_count != v.instance_count ? 1 : 0;
+        for(size_t i = 0; !diff && i < v.instance_count; ++i)
+            diff += memcmp(&v.instances[i].m, &vB.instances[i].m, sizeof(ptg_mesh)) ||
+                    memcmp(&v.instances[i].transform, &vB.instances[i].transform, 2 * sizeof(v.instances[i].transform));
+        BlockCache cB;
+        FramePack fB;
+        if(cB.pack_frame(vB.nodes, vB.links, vB.static_node_count, vB.index_count, vB.vertex_count, vB.subframes,
+                         vB.subframe_count, vB.instances, vB.instance_count, vB.nodes + vB.static_node_count,
+                         vB.links + 8 * vB.static_node_count, vB.static_node_count, vB.node_count - vB.static_node_count, fB, err))
+        { fprintf(stderr, "ANYHIER pack: %s\n", err.c_str()); return 1; }
+        pkB.E = fB.new_blas;
+        pkB.E.insert(pkB.E.end(), fB.tlas.begin(), fB.tlas.end());
+        pkB.inst_root = fB.inst_root;
+        pkB.tlas_root = fB.tlas_root;
+        printf("ANYHIER cost %s: static nodes %zu (reference %zu); BLAS blocks %.1f MB (reference %.1f MB); instances differing %zu\n",
+               hc, vB.static_node_count, v.static_node_count, fB.new_blas.size() * 128 / 1e6,
+               (cache.blas.size() + fp.new_blas.size()) * 128 / 1e6, diff);
+        if(diff) return 1;
+#else
+        fprintf(stderr, "ANYHIER needs the walk_simh build (tools/Makefile)\n");
+        return 2;
+#endif
+    }
+
     // the query mix
     std::vector<Query> qs;
     const bool tiled = getenv("CACHESIM") != nullptr;   // paths in the device's queue order: 8 pixels x 8 samples per wave
@@ -1300,12 +1345,18 @@ int main(int argc, char** argv)
         }
         return 0;
     }
-    Stats sl[2], sb[2];
-    uint64_t mism = 0;
+    Stats sl[2], sb[2], sh;
+    uint64_t mism = 0, mismh = 0;
     for(const Query& q: qs)
     {
         Res a = link_walk(v, q, sl[q.any]);
         Res b = block_walk(v, pk, q, sb[q.any], S);
+        if(sceneB && q.any)
+        {
+            const Res c = block_walk(vB, pkB, q, sh, S);
+            if(!(a == c) && mismh++ < 5)
+                fprintf(stderr, "ANYHIER mismatch: link occ=%d | rebuilt occ=%d\n", a.occluded, c.occluded);
+        }
         if(getenv("CLOSEBOUND") && !q.any && b.inst != 0xFFFFFFFFu)
         {   // model: the closest-hit walk started with tmax = next float above the
             // final hit's t (a perfect neighbour candidate); same result, fewer steps?
@@ -1353,6 +1404,18 @@ int main(int argc, char** argv)
         }
         printf("\n");
     }
+    if(sceneB)
+    {
+        const Stats& b = sb[1];
+        printf("ANYHIER any-hit over the rebuilt BLASes: %llu mismatches vs the link walk\n", (unsigned long long)mismh);
+        printf("  reference tree: boxes %.1f  steps %.2f (block %.2f, leaf %.2f)  tri %.2f  enters %.2f  iters %.1f  bytes %.0f\n",
+               b.visits / b.queries, b.steps / b.queries, b.block_steps / b.queries, b.leaf_steps / b.queries, b.tri / b.queries,
+               b.enters / b.queries, b.iters / b.queries, b.bytes / b.queries);
+        printf("  rebuilt tree  : boxes %.1f  steps %.2f (block %.2f, leaf %.2f)  tri %.2f  enters %.2f  iters %.1f  bytes %.0f\n",
+               sh.visits / sh.queries, sh.steps / sh.queries, sh.block_steps / sh.queries, sh.leaf_steps / sh.queries,
+               sh.tri / sh.queries, sh.enters / sh.queries, sh.iters / sh.queries, sh.bytes / sh.queries);
+        ptg_scene_destroy(sceneB);
+    }
     ptg_scene_destroy(scene);
-    return mism ? 1 : 0;
+    return (mism || mismh) ? 1 : 0;
 }
