@@ -149,11 +149,15 @@ def main():
     if a.metric:
         w, h = 1280, 720
         res = json.load(open(a.out)) if os.path.exists(a.out) else {}
-        res["metric_config"] = {"width": w, "height": h, "spp": a.spp, "bounces": BOUNCES,
-                                "frames": [metric_stats(assets, f, w, h, a.spp) for f in a.frames]}
-        with open(a.out, "w") as f:
-            json.dump(res, f, indent=1)
-        print(json.dumps(res["metric_config"], indent=1))
+        rows = res.setdefault("metric_config", {"width": w, "height": h, "bounces": BOUNCES, "rows": []})["rows"]
+        for f in a.frames:
+            st = metric_stats(assets, f, w, h, a.spp)
+            st["spp"] = a.spp
+            rows[:] = [r for r in rows if (r["frame"], r["spp"]) != (f, a.spp)] + [st]
+            rows.sort(key=lambda r: (r["spp"], r["frame"]))
+            with open(a.out, "w") as fh:
+                json.dump(res, fh, indent=1)
+            print(json.dumps(st, indent=1))
         return
     res = {"config": {"width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
                       "builds": {"strict": "-O2 -ffp-contract=off -fno-fast-math (== the GPU path, bit for bit)",
