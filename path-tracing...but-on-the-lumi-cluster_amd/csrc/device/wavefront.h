@@ -215,8 +215,14 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     // bounce `round` (path_tracer.hh:699-720): NEE setup, BSDF sample, next ray
     const Material M{info.albedo, info.roughness, info.metallic, info.transmission, info.eta};
     const f3 view = tangent_view(p.ray_d, info);
-    // a shadow ray whose outcome cannot change the result is not traced (nee_shadow_moot)
-    const bool pending = nee_prepare(seed, L, info, M, view, p.nee, mp) && !nee_shadow_moot(p.nee, info.pos);
+    // a shadow ray whose outcome cannot change the result is not traced: the
+    // sun ray is below the ground (nee_shadow_moot), or the path's throughput
+    // is zero (nee_term_moot)
+#ifndef PTG_ZERO_ATT_MOOT
+#define PTG_ZERO_ATT_MOOT 1
+#endif
+    const bool pending = nee_prepare(seed, L, info, M, view, p.nee, mp) && !nee_shadow_moot(p.nee, info.pos) &&
+                         !(PTG_ZERO_ATT_MOOT && nee_term_moot(p.att, p.contrib, p.nee));
     const f4 ub = uniform4(seed);
     f3 tdir, batt;
     float bpdf;
