@@ -1682,6 +1682,32 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
 {
     const float mis_pdf = bpdf < 0 ? -bpdf : (info.nee_pdf * info.nee_pdf + bpdf * bpdf) / bpdf;
     attenuation = attenuation * batt;
+#ifndef PTG_ZERO_ATT_SKY
+#define PTG_ZERO_ATT_SKY 1
+#endif
+    if constexpr(!NEED_REG && PTG_ZERO_ATT_SKY)
+    {   // The path retires here (the sky pass: its ray left the scene).  With
+        // the throughput exactly +-0 in every component the term is
+        // att * X / mis_pdf with X = insc + (aatt * albedo) * emission finite
+        // and without a sign bit: the in-scatter and the transmittance are
+        // sums and products of exp values (nishita_atmosphere_scattering,
+        // path_tracer.hh:499-588: a shadowed step's infinite optical depth
+        // only feeds an attenuation that is then set to 0), the albedo is
+        // the sun-disk term (visible * colour) * w >= +0 for a colour without
+        // sign bits, the emission 1.  So att * X is att * (+0) bit for bit
+        // (+-0 with att's signs), and with mis_pdf finite and nonzero the
+        // contribution takes the same bits without the integrals; their one
+        // random draw only feeds this retired path.
+        const uint32_t az = (__float_as_uint(attenuation.x) | __float_as_uint(attenuation.y) |
+                             __float_as_uint(attenuation.z)) & 0x7FFFFFFFu;
+        const uint32_t colour_signs = (__float_as_uint(L.color.x) | __float_as_uint(L.color.y) |
+                                       __float_as_uint(L.color.z)) >> 31;
+        if(az == 0u && colour_signs == 0u && __builtin_isfinite(mis_pdf) && mis_pdf != 0.0f)
+        {
+            contribution = contribution + (attenuation * V3(0.0f, 0.0f, 0.0f)) / mis_pdf;
+            return;
+        }
+    }
     f3 aatt, insc;
     atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc, mp);
     const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
