@@ -194,7 +194,11 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     if(round == 0)
     {   // primary ray (path_tracer.hh:686-693)
         f3 attenuation, in_scatter;
-        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter, mp);
+        // the sky pass (KIND 2) retires the path: an albedo of +0 (the sun disk
+        // missed) lets a fully shadowed sky skip its integrals (atmosphere_scattering)
+        const bool zero_albedo = KIND == 2 && (__float_as_uint(info.albedo.x) | __float_as_uint(info.albedo.y) |
+                                               __float_as_uint(info.albedo.z)) == 0u;
+        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter, mp, zero_albedo);
         p.att = attenuation;
         p.contrib = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
         p.reg = 1.0f;
@@ -232,6 +236,16 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     p.batt = batt;
     p.bpdf = bpdf;
     p.seed = to_uint4(seed);
+#ifndef PTG_ZERO_ATT_RETIRE
+#define PTG_ZERO_ATT_RETIRE 1
+#endif
+    if(PTG_ZERO_ATT_RETIRE && round + 1 == sc.max_bounces && !pending && sc.attrs_finite &&
+       last_bounce_moot(p.att, batt, bpdf, p.contrib, L))
+    {   // the last bounce would add +-0 terms only: the contribution is final
+        if(MP::kFast && mp.fail_mask) return SH_REDO;
+        st_out(out_samples + p.meta.x, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f));
+        return SH_DONE;
+    }
     p.meta.y = meta_pack(round + 1, pending, meta_sub(p.meta));
     if(MP::kFast && mp.fail_mask) return SH_REDO;
     return SH_CONTINUE;

@@ -943,6 +943,7 @@ struct ptg_context {
     size_t block_count = 0, subframe_count = 0, instance_count = 0;
     uint32_t stack_bound = 0;                            // TLAS + BLAS stack bound of this frame (entries)
     float cell_lo[3] = {0, 0, 0}, cell_scale[3] = {0, 0, 0};   // hit-cell grid (PTG_CELL_SORT)
+    bool attrs_finite = false;                           // every vertex albedo / material value finite
     std::vector<uint32_t> host_tlas_root;
     std::vector<ptg_subframe> host_subframes;
     bool frame_ready = false;
@@ -1069,6 +1070,7 @@ struct ptg_context {
         s.tri_count = uint32_t(index_count / 3);
         s.inst_count = uint32_t(instance_count);
         s.debug = PTG_DEBUG ? debug.as<uint32_t>() : nullptr;
+        s.attrs_finite = attrs_finite ? 1u : 0u;
         for(int k = 0; k < 3; ++k)
         {
             s.cell_lo[k] = cell_lo[k];
@@ -1622,6 +1624,14 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     PTG_HIP(hipMemcpyAsync(ctx->albedo.p, albedo, vertex_count * 16, hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->material.p, material, vertex_count * 16, hipMemcpyHostToDevice, s));
     PTG_HIP(hipStreamSynchronize(s));
+    // whether every vertex albedo and material value is finite: the surface
+    // pass retires a zero-throughput path at its last bounce only then
+    // (last_bounce_moot: the term it skips is att * X with X made of them)
+    ctx->attrs_finite = true;
+    for(size_t i = 0; i < vertex_count && ctx->attrs_finite; ++i)
+        ctx->attrs_finite = std::isfinite(albedo[i].x) && std::isfinite(albedo[i].y) && std::isfinite(albedo[i].z) &&
+                            std::isfinite(albedo[i].w) && std::isfinite(material[i].x) && std::isfinite(material[i].y) &&
+                            std::isfinite(material[i].z) && std::isfinite(material[i].w);
     ctx->static_nodes = node_count;
     ctx->index_count = index_count;
     ctx->vertex_count = vertex_count;
