@@ -80,7 +80,6 @@ struct DevScene {
     uint2* spill;                  // LdsStack spill areas, spill_stride entries per walk lane
     uint32_t spill_stride;
     uint32_t* debug;               // PTG_DEBUG: violation counters (kDebug* slots), else null
-    float cell_lo[3], cell_scale[3];   // the hit-cell grid of the frame's scene box (k_wf_classify's sort key)
     uint32_t attrs_finite;         // every vertex albedo / material value finite (last_bounce_moot)
 };
 

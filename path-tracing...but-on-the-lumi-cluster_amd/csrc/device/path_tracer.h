@@ -1461,7 +1461,7 @@ template<class MP> PTG_D f3 atmosphere_attenuation(float jitter, f3 pos, f3 view
 // nishita_atmosphere_scattering (:499-588)
 template<class MP>
 PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, float tmax, f3& attenuation, f3& in_scatter,
-                                 MP& mp, bool zero_albedo = false)
+                                 MP& mp)
 {
     const f3 earth = V3(0, -EARTH_RADIUS, 0);
     attenuation = V3(1.0f, 1.0f, 1.0f);
@@ -1473,41 +1473,6 @@ PTG_D void atmosphere_scattering(u4& seed, const Light& L, f3 pos, f3 view, floa
     tmax = gmin(atmax, tmax < 0 ? MAX_RAY_DIST : tmax);
     const float segment = (tmax - tmin) / (float)PRIMARY_ITERATIONS;
     const f4 jitter = uniform4(seed);
-#ifndef PTG_DARK_SKY
-#define PTG_DARK_SKY 1
-#endif
-    if(PTG_DARK_SKY && zero_albedo)
-    {   // The caller's X = in_scatter + (attenuation * albedo) * emission with
-        // an albedo of +0 (a sky ray that misses the sun disk, hit_info): when
-        // every primary step's light ray is shadowed (below the ground, the
-        // reference's `shadowed`), every local attenuation is 0, the sums are
-        // +0 and in_scatter is ((+0 * R) * phase + (+0 * M) * phase) * colour
-        // * 4, i.e. (+0 * colour) * 4; X is then +0 whatever the attenuation
-        // (finite, >= 0), which nothing else of this retiring path reads.  The
-        // shadow tests alone (no exp) decide it, on the same tmin / tmax
-        // state the loop below carries; the first lit step ends the test.
-        float t0 = tmin, t1 = tmax;
-        bool all = true;
-        for(int i = 0; i < PRIMARY_ITERATIONS && all; ++i)
-        {
-            const float t = segment * (jitter.x + (float)i);
-            const f3 p = pos + t * view;
-            ray_sphere(p, L.dir, earth, EARTH_RADIUS + ATMOSPHERE_HEIGHT, t0, t1);   // keeps old values on a miss
-            const float light_segment = (t1 - t0) / (float)SECONDARY_ITERATIONS;
-            bool shadowed = false;
-            for(int j = 0; j < SECONDARY_ITERATIONS; ++j)
-            {
-                const float tt = light_segment * (jitter.y + (float)j);
-                if(length((p + tt * L.dir) - earth) - EARTH_RADIUS < 0) shadowed = true;
-            }
-            all = shadowed;
-        }
-        if(all)
-        {
-            in_scatter = (V3(0.0f, 0.0f, 0.0f) * L.color) * 4.0f;
-            return;   // attenuation stays (1, 1, 1): it meets only the +0 albedo
-        }
-    }
     const float mu = dot(view, L.dir);
     const float rayleigh_phase = 3.0f / (16.0f * PI_F) * (1.0f + mu * mu);
     const float g = MIE_ANISOTROPY;
@@ -1768,10 +1733,7 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
         }
     }
     f3 aatt, insc;
-    // (the retiring sky pass: an albedo of +0 lets a fully shadowed sky skip its integrals)
-    const bool zero_albedo = !NEED_REG && (__float_as_uint(info.albedo.x) | __float_as_uint(info.albedo.y) |
-                                           __float_as_uint(info.albedo.z)) == 0u;
-    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc, mp, zero_albedo);
+    atmosphere_scattering(seed, L, ray_o, ray_dir, info.thit, aatt, insc, mp);
     const f3 term = attenuation * (insc + (aatt * info.albedo) * info.emission);
     contribution = contribution + term / mis_pdf;
     attenuation = attenuation * (aatt / fabsf(bpdf));

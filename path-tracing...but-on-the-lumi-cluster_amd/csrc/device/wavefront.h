@@ -97,21 +97,8 @@ template<typename T> PTG_D void st_state(T* p, T value)
 template<typename T> PTG_D T ld_out(const T* p) { return ld_state(p); }
 template<typename T> PTG_D void st_out(T* p, T value) { st_state(p, value); }
 
-#ifndef PTG_PACK_BATT
-#define PTG_PACK_BATT 0
-#endif
-// PTG_PACK_BATT: the bounce's bsdf attenuation rides in the spare w words of
-// meta, ray_o and ray_d (16 B less path state per path read and written)
 PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
 {
-#if PTG_PACK_BATT
-    st_state(S.meta + q, make_uint4(p.meta.x, p.meta.y, p.meta.z, __float_as_uint(p.batt.x)));
-    st_state(S.seed + q, p.seed);
-    st_state(S.ray_o + q, make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, p.batt.y));
-    st_state(S.ray_d + q, make_float4(p.ray_d.x, p.ray_d.y, p.ray_d.z, p.batt.z));
-    st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
-    st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
-#else
     st_state(S.meta + q, p.meta);
     st_state(S.seed + q, p.seed);
     st_state(S.ray_o + q, make_float4(p.ray_o.x, p.ray_o.y, p.ray_o.z, 0.f));
@@ -119,7 +106,6 @@ PTG_D void store_path(const PathSoA& S, uint32_t q, const PathRec& p)
     st_state(S.att + q, make_float4(p.att.x, p.att.y, p.att.z, p.reg));
     st_state(S.contrib + q, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.bpdf));
     st_state(S.batt + q, make_float4(p.batt.x, p.batt.y, p.batt.z, 0.f));
-#endif
     if(!meta_nee(p.meta)) return;   // no pending NEE ray: its records are never read
     st_state(S.nee_c + q, make_float4(p.nee.color.x, p.nee.color.y, p.nee.color.z, p.nee.mis_pdf));
     st_state(S.nee_d + q, make_float4(p.nee.dir.x, p.nee.dir.y, p.nee.dir.z, p.nee.jitter));
@@ -157,11 +143,7 @@ PTG_D PathRec load_path(const PathSoA& S, uint32_t q, bool carried = true)
     p.reg = a.w;
     p.contrib = xyz(c);
     p.bpdf = c.w;
-#if PTG_PACK_BATT
-    p.batt = V3(__uint_as_float(p.meta.w), ro.w, rd.w);
-#else
     p.batt = xyz(ld_state(S.batt + q));
-#endif
     p.nee.color = xyz(nc);
     p.nee.mis_pdf = nc.w;
     p.nee.dir = xyz(nd);
@@ -194,11 +176,7 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     if(round == 0)
     {   // primary ray (path_tracer.hh:686-693)
         f3 attenuation, in_scatter;
-        // the sky pass (KIND 2) retires the path: an albedo of +0 (the sun disk
-        // missed) lets a fully shadowed sky skip its integrals (atmosphere_scattering)
-        const bool zero_albedo = KIND == 2 && (__float_as_uint(info.albedo.x) | __float_as_uint(info.albedo.y) |
-                                               __float_as_uint(info.albedo.z)) == 0u;
-        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter, mp, zero_albedo);
+        atmosphere_scattering(seed, L, p.ray_o, p.ray_d, info.thit, attenuation, in_scatter, mp);
         p.att = attenuation;
         p.contrib = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
         p.reg = 1.0f;

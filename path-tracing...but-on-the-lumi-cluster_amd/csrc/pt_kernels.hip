@@ -163,27 +163,6 @@ __device__ __forceinline__ void tally_redo(unsigned long long* tally, int kind, 
 
 // ---- wavefront pipeline (csrc/device/wavefront.h) ----
 
-// PTG_CELL_SORT: k_wf_classify orders each tile's surface hits by the cell of
-// their hit position (an 8 x 8 x 8 grid over the frame's scene box, Morton
-// order), written by the closest-hit walk into the hit record's spare bits
-#ifndef PTG_CELL_SORT
-#define PTG_CELL_SORT 0
-#endif
-#if PTG_CELL_SORT
-constexpr uint32_t kCells = 512;
-__device__ __forceinline__ uint32_t spread3(uint32_t v)   // 3 bits -> every third bit
-{
-    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
-}
-__device__ __forceinline__ uint32_t hit_cell(const DevScene& sc, f3 p)
-{
-    const float fx = (p.x - sc.cell_lo[0]) * sc.cell_scale[0], fy = (p.y - sc.cell_lo[1]) * sc.cell_scale[1],
-                fz = (p.z - sc.cell_lo[2]) * sc.cell_scale[2];
-    const uint32_t cx = uint32_t(fminf(fmaxf(fx, 0.0f), 7.0f)), cy = uint32_t(fminf(fmaxf(fy, 0.0f), 7.0f)),
-                   cz = uint32_t(fminf(fmaxf(fz, 0.0f), 7.0f));
-    return spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
-}
-#endif
 
 // Lane -> (pixel, sample) of a chunk: a wave holds 8 pixels x 8 consecutive
 // samples (one motion-blur subframe); consecutive waves walk the sample
@@ -344,12 +323,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
         else
         {
             const Hit h = w.result();
-            // w: back_face in bit 31; PTG_CELL_SORT: the hit position's cell (k_wf_classify's sort key)
-            uint32_t cw = h.back_face ? 0x80000000u : 0u;
-#if PTG_CELL_SORT
-            if(h.instance_id != 0xFFFFFFFFu) cw |= hit_cell(sc, w.cold.world_o() + w.cold.world_d() * h.thit);
-#endif
-            nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, cw));
+            nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
             if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
                 nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
         }
@@ -484,100 +458,46 @@ __global__ __launch_bounds__(kBlock) void k_wf_classify(const uint32_t* __restri
     // kernel's time.
     constexpr uint32_t kSub = 8, kTile = kSub * kBlock;
     const uint32_t n = counts[2 * round];
-#if PTG_CELL_SORT
-    // bins: 0 sky, 1 sky with a pending NEE ray, then the hits by (NEE
-    // pending, cell of the hit position in Morton order): a shade block then
-    // takes nearby paths, and so do the next round's waves it fills
-    constexpr uint32_t kBins = 2 + 2 * kCells;
-    __shared__ uint32_t bin_count[kBins], bin_start[kBins];
-    __shared__ uint32_t wave_sum_lds[kBlock / 64];
-#else
-    constexpr uint32_t kBins = 4;
-    __shared__ uint32_t bin_count[kBins];
-#endif
+    __shared__ uint32_t bin_count[4];
     __shared__ unsigned long long base2;
     for(uint32_t tile = blockIdx.x * kTile; tile < n; tile += gridDim.x * kTile)
     {
-        for(uint32_t b = threadIdx.x; b < kBins; b += kBlock) bin_count[b] = 0;
+        if(threadIdx.x < 4) bin_count[threadIdx.x] = 0;
         __syncthreads();
         uint32_t key[kSub], rank[kSub];
 #pragma unroll
         for(uint32_t k = 0; k < kSub; ++k)
         {
             const uint32_t q = tile + k * kBlock + threadIdx.x;
-            key[k] = 0xFFFFFFFFu;
+            key[k] = 4u;
             rank[k] = 0;
             if(q < n)
             {
-#if PTG_CELL_SORT
-                const uint4 hv = tr.hit[q];
-                const bool hit = __uint_as_float(hv.x) > 0.0f;
-#else
                 const bool hit = __uint_as_float(tr.hit[q].x) > 0.0f;
-#endif
                 // shade(round-1) wrote 1 for survivors without a pending NEE ray,
                 // the shadow walk 0/1 for those with one (meta is not read)
                 const bool nee = round > 0 && tr.shadow[q] == 0;
-#if PTG_CELL_SORT
-                key[k] = hit ? 2u + (nee ? kCells : 0u) + (hv.w & (kCells - 1u)) : (nee ? 1u : 0u);
-#else
                 key[k] = (hit ? 2u : 0u) | (nee ? 1u : 0u);
-#endif
                 rank[k] = atomicAdd(&bin_count[key[k]], 1u);
             }
         }
         __syncthreads();
-#if PTG_CELL_SORT
-        {   // exclusive scan of the hit bins: each thread sums kPer consecutive bins
-            constexpr uint32_t kPer = (2 * kCells) / kBlock;
-            static_assert(kPer * kBlock == 2 * kCells, "hit bins a multiple of the block");
-            uint32_t loc[kPer], sum = 0;
-#pragma unroll
-            for(uint32_t i = 0; i < kPer; ++i) { loc[i] = bin_count[2 + threadIdx.x * kPer + i]; sum += loc[i]; }
-            const uint32_t lane = threadIdx.x & 63u;
-            uint32_t incl = sum;
-#pragma unroll
-            for(uint32_t o = 1; o < 64; o <<= 1)
-            {
-                const uint32_t v = __shfl_up(incl, o);
-                if(lane >= o) incl += v;
-            }
-            if(lane == 63) wave_sum_lds[threadIdx.x >> 6] = incl;
-            __syncthreads();
-            uint32_t off = incl - sum;
-            for(uint32_t w2 = 0; w2 < (threadIdx.x >> 6); ++w2) off += wave_sum_lds[w2];
-#pragma unroll
-            for(uint32_t i = 0; i < kPer; ++i) { bin_start[2 + threadIdx.x * kPer + i] = off; off += loc[i]; }
-            if(threadIdx.x == 0)
-            {
-                uint32_t nhit = 0;
-                for(uint32_t w2 = 0; w2 < kBlock / 64; ++w2) nhit += wave_sum_lds[w2];
-                const unsigned long long nsky = bin_count[0] + bin_count[1];
-                base2 = atomicAdd(reinterpret_cast<unsigned long long*>(lcounts), (nsky << 32) | nhit);
-            }
-        }
-#else
         if(threadIdx.x == 0)
         {
             const unsigned long long nsky = bin_count[0] + bin_count[1], nhit = bin_count[2] + bin_count[3];
             base2 = atomicAdd(reinterpret_cast<unsigned long long*>(lcounts), (nsky << 32) | nhit);
         }
-#endif
         __syncthreads();
         const uint32_t hit_base = uint32_t(base2), sky_base = uint32_t(base2 >> 32);
 #pragma unroll
         for(uint32_t k = 0; k < kSub; ++k)
         {
             const uint32_t q = tile + k * kBlock + threadIdx.x;
-            if(key[k] == 0xFFFFFFFFu) continue;
-#if PTG_CELL_SORT
-            if(key[k] >= 2u) hit_list[hit_base + bin_start[key[k]] + rank[k]] = q;
-#else
+            if(key[k] == 4u) continue;
             if(key[k] & 2u) hit_list[hit_base + (key[k] == 3u ? bin_count[2] : 0u) + rank[k]] = q;
-#endif
             else sky_list[sky_base + (key[k] == 1u ? bin_count[0] : 0u) + rank[k]] = q;
         }
-        __syncthreads();   // the bins are rewritten by the next tile
+        __syncthreads();   // bin_count is rewritten by the next tile
     }
 }
 
@@ -606,7 +526,7 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
     h.thit = __uint_as_float(hv.x);
     h.instance_id = hv.y;
     h.primitive_id = hv.z;
-    h.back_face = (hv.w >> 31) != 0;
+    h.back_face = hv.w != 0;
     h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
 }
 
@@ -942,7 +862,6 @@ struct ptg_context {
     uint32_t stage_next = 0;
     size_t block_count = 0, subframe_count = 0, instance_count = 0;
     uint32_t stack_bound = 0;                            // TLAS + BLAS stack bound of this frame (entries)
-    float cell_lo[3] = {0, 0, 0}, cell_scale[3] = {0, 0, 0};   // hit-cell grid (PTG_CELL_SORT)
     bool attrs_finite = false;                           // every vertex albedo / material value finite
     std::vector<uint32_t> host_tlas_root;
     std::vector<ptg_subframe> host_subframes;
@@ -1071,11 +990,6 @@ struct ptg_context {
         s.inst_count = uint32_t(instance_count);
         s.debug = PTG_DEBUG ? debug.as<uint32_t>() : nullptr;
         s.attrs_finite = attrs_finite ? 1u : 0u;
-        for(int k = 0; k < 3; ++k)
-        {
-            s.cell_lo[k] = cell_lo[k];
-            s.cell_scale[k] = cell_scale[k];
-        }
         return s;
     }
 };
@@ -1825,16 +1739,6 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     ctx->packed_mesh.insert(new_mesh.begin(), new_mesh.end());
     ctx->block_count = fp.total_blocks();
     ctx->stack_bound = fp.stack_bound();
-    {   // the hit-cell grid (PTG_CELL_SORT's sort key): subframe 0's TLAS root box in 8 cells per axis
-        const ptg_bvh_node& root = frame_nodes[size_t(subframes[0].tlas.node_offset) - first_node];
-        const float lo[3] = {root.min_x, root.min_y, root.min_z}, hi[3] = {root.max_x, root.max_y, root.max_z};
-        for(int k = 0; k < 3; ++k)
-        {
-            const float ext = hi[k] - lo[k];
-            ctx->cell_lo[k] = std::isfinite(lo[k]) ? lo[k] : 0.0f;
-            ctx->cell_scale[k] = (std::isfinite(ext) && ext > 0.0f) ? 8.0f / ext : 0.0f;
-        }
-    }
     ctx->host_tlas_root = fp.tlas_root;
     ctx->subframe_count = subframe_count;
     ctx->instance_count = instance_count;
