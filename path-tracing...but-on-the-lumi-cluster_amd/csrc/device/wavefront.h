@@ -184,11 +184,16 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
         // return: insc +0, aatt 1; finite vertex data), so the term is
         // (att * batt) * (+0) whatever surface it is - the hit's shading
         // (indices, normals, albedo, material) is not fetched.  nee_pdf is 0
-        // for a hit (hit_info).  The path retires.  (Counted as a shade, as
-        // hit_info counts it.)
-        if(COUNT) cnt.shades++;
+        // for a hit (hit_info).  The path retires.  (Counted as a shade only
+        // when it finishes an NEE term: the counter's shades are the shading
+        // passes that evaluate the double library, which the exact redo pass
+        // repeats, tests/test_gpu_redo.py.)
         f3 nee = V3(0, 0, 0);
-        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o, mp);
+        if(meta_nee(p.meta) && !occluded)
+        {
+            if(COUNT) cnt.shades++;
+            nee = nee_finish(p.nee, p.ray_o, mp);
+        }
         p.contrib = p.contrib + p.att * nee;
         const float zero_pdf = 0.0f;
         const float mis_pdf = p.bpdf < 0 ? -p.bpdf : (zero_pdf * zero_pdf + p.bpdf * p.bpdf) / p.bpdf;
