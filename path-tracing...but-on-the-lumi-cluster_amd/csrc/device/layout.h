@@ -38,9 +38,7 @@ static_assert(sizeof(InstTrav) == 64, "InstTrav is four 16-byte loads");
 
 struct alignas(16) InstShade {
     float rot[9];              // transform.r[k].{x,y,z} for k = 0..2
-    uint32_t index_offset, base_vertex_offset;
-    uint32_t emissive;         // 1: a triangle of the mesh names a vertex whose emission (material.w) is not +-0
-    uint32_t pad[4];
+    uint32_t index_offset, base_vertex_offset, pad[5];
 };
 static_assert(sizeof(InstShade) == 64, "InstShade is four 16-byte loads");
 

@@ -172,37 +172,12 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
     const Light L = light_of(sf);
     const uint32_t round = meta_round(p.meta);
     u4 seed = to_u4(p.seed);
-#ifndef PTG_DARK_LAST_HIT
-#define PTG_DARK_LAST_HIT 1
-#endif
-    if(PTG_DARK_LAST_HIT && KIND == 1 && round == sc.max_bounces && round > 0 && sc.attrs_finite && h.thit < 1e3f &&
-       sc.inst_shade[h.instance_id].emissive == 0u)
-    {   // The last bounce's ray hit a surface without emission (InstShade::
-        // emissive 0) nearer than 1e3: the reference's bounce tail then adds
-        // (att * batt) * X / mis_pdf with X = insc + (aatt * albedo) *
-        // emission = (+0) + (1 * albedo) * (+-0) = +0 (the atmosphere's early
-        // return: insc +0, aatt 1; finite vertex data), so the term is
-        // (att * batt) * (+0) whatever surface it is - the hit's shading
-        // (indices, normals, albedo, material) is not fetched.  nee_pdf is 0
-        // for a hit (hit_info).  The path retires.  (Counted as a shade only
-        // when it finishes an NEE term: the counter's shades are the shading
-        // passes that evaluate the double library, which the exact redo pass
-        // repeats, tests/test_gpu_redo.py.)
+    if(round > 0)
+    {   // end of bounce round-1: its NEE term (it reads nothing of the hit, so
+        // it runs before the hit's shading: fewer registers live across it)
         f3 nee = V3(0, 0, 0);
-        if(meta_nee(p.meta) && !occluded)
-        {
-            if(COUNT) cnt.shades++;
-            nee = nee_finish(p.nee, p.ray_o, mp);
-        }
+        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o, mp);
         p.contrib = p.contrib + p.att * nee;
-        const float zero_pdf = 0.0f;
-        const float mis_pdf = p.bpdf < 0 ? -p.bpdf : (zero_pdf * zero_pdf + p.bpdf * p.bpdf) / p.bpdf;
-        const f3 att = p.att * p.batt;
-        const f3 term = att * V3(0.0f, 0.0f, 0.0f);
-        p.contrib = p.contrib + term / mis_pdf;
-        if(MP::kFast && mp.fail_mask) return SH_REDO;
-        st_out(out_samples + p.meta.x, make_float4(p.contrib.x, p.contrib.y, p.contrib.z, 0.f));
-        return SH_DONE;
     }
     HitInfo info = hit_info<COUNT, KIND>(sc, L, p.ray_o, p.ray_d, h, cnt);
     if(round == 0)
@@ -213,13 +188,8 @@ PTG_D ShadeResult shade_path(const DevScene& sc, PathRec& p, const Hit& h, bool 
         p.contrib = V3(0, 0, 0) + (in_scatter + (attenuation * info.albedo) * info.emission);
         p.reg = 1.0f;
     }
-    else
-    {   // end of bounce round-1: its NEE term, then the bounce ray's tail
-        f3 nee = V3(0, 0, 0);
-        if(meta_nee(p.meta) && !occluded) nee = nee_finish(p.nee, p.ray_o, mp);
-        p.contrib = p.contrib + p.att * nee;
+    else   // the bounce ray's tail
         bounce_tail<MP, KIND != 2>(seed, L, p.ray_o, p.ray_d, info, p.batt, p.bpdf, p.att, p.contrib, p.reg, mp);
-    }
     if(KIND == 2 || !(round < sc.max_bounces && info.thit > 0))
     {
         if(MP::kFast && mp.fail_mask) return SH_REDO;

@@ -850,11 +850,6 @@ struct ptg_context {
     // (bvh.cc:243-246), so a candidate triangle's leaf box can be computed from
     // its vertices (k_wf_walk<ANY>); checked once per pair on the host
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, bool> leaf_bounds_ok;
-    // per vertex: whether its emission (material.w) is anything but +-0; per
-    // (index offset, triangle count, base vertex) whether a triangle of the
-    // mesh names such a vertex (InstShade::emissive)
-    std::vector<uint8_t> host_emits;
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, bool> mesh_emits;
     size_t static_nodes = 0, index_count = 0, vertex_count = 0;
     std::unordered_set<uint32_t> packed_mesh;
     // BLAS blocks packed so far (host copy; their device copy leads `blocks`)
@@ -1520,14 +1515,6 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
         ctx->host_indices.assign(indices, indices + index_count);
         ctx->host_pos.assign(pos, pos + vertex_count);
         ctx->leaf_bounds_ok.clear();
-        ctx->mesh_emits.clear();
-        ctx->host_emits.resize(vertex_count);
-        for(size_t i = 0; i < vertex_count; ++i)
-        {
-            uint32_t b;
-            memcpy(&b, &material[i].w, 4);
-            ctx->host_emits[i] = (b & 0x7FFFFFFFu) != 0u;
-        }
     }
     catch(const std::bad_alloc&)
     {
@@ -1609,23 +1596,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
         }
         is[i].index_offset = in.m.index_offset;
         is[i].base_vertex_offset = in.m.base_vertex_offset;
-        std::fill(is[i].pad, is[i].pad + 4, 0u);
-        {   // whether a triangle of its mesh names a vertex with emission (ranges checked by pack_frame)
-            const auto key = std::make_tuple(in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset);
-            auto e = ctx->mesh_emits.find(key);
-            if(e == ctx->mesh_emits.end())
-            {
-                bool any = false;
-                const size_t i0 = in.m.index_offset, i1 = std::min(ctx->host_indices.size(), i0 + size_t(in.m.triangle_count) * 3);
-                for(size_t k = i0; k < i1 && !any; ++k)
-                {
-                    const size_t v = size_t(in.m.base_vertex_offset) + ctx->host_indices[k];
-                    any = v >= ctx->host_emits.size() || ctx->host_emits[v];   // (out of range: never claimed dark)
-                }
-                e = ctx->mesh_emits.emplace(key, any).first;
-            }
-            is[i].emissive = e->second ? 1u : 0u;
-        }
+        std::fill(is[i].pad, is[i].pad + 5, 0u);
         if(!ctx->packed_mesh.count(in.m.index_offset) && new_mesh.insert(in.m.index_offset).second)
             mesh_jobs.push_back(MeshJob{in.m.index_offset, in.m.triangle_count, in.m.base_vertex_offset, 0});
     }

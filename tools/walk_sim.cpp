@@ -225,6 +225,7 @@ struct SimWalker {
     bool spec;
     uint32_t skip = 0xFFFFFFFFu;   // OCC model: an instance not to enter (walked first already)
     double tl_steps = 0, blas_cur = 0, enters_n = 0;   // OCC model: TLAS block steps, steps in the current BLAS, entries
+    double first_confirm_steps = -1;                     // FIRSTHIT model: st.steps when the first hit was confirmed
 
     SimWalker(const ptg_scene_view& v_, const Packed& pk_, const Query& q_, Stats& st_, uint32_t C_, bool spec_)
         : v(v_), pk(pk_), q(q_), st(st_), C(C_), spec(spec_)
@@ -411,6 +412,7 @@ struct SimWalker {
             if(q.any) { best.occluded = true; best.occ_inst = b.id; best.occ_prim = id; return 2; }
             best = c;
             tmax = c.t;
+            if(first_confirm_steps < 0) first_confirm_steps = st.steps;
         }
         return 0;
     }
@@ -476,6 +478,22 @@ Res block_walk(const ptg_scene_view& v, const Packed& pk, const Query& q, Stats&
     }
     st.depth_hist[w.maxd]++;
     g_max_query_steps = std::max(g_max_query_steps, st.steps - steps0);
+    if(getenv("FIRSTHIT") && !q.any)
+    {   // model: a closest-hit walk that may stop at its first confirmed hit
+        // (the last bounce when no emissive instance can be hit): steps to that
+        // hit against the whole walk, for bounce rays (round >= 1)
+        static double all = 0, upto = 0, n = 0, nh = 0;
+        if(q.round >= 1)
+        {
+            all += st.steps - steps0;
+            upto += w.first_confirm_steps >= 0 ? w.first_confirm_steps - steps0 : st.steps - steps0;
+            n += 1;
+            nh += w.first_confirm_steps >= 0;
+            if(uint64_t(n) % 20000 == 0)
+                fprintf(stderr, "FIRSTHIT: %.0f bounce queries (%.1f%% hit): steps %.2f, to the first confirm %.2f (%.1f%%)\n", n,
+                        100 * nh / n, all / n, upto / n, 100 * upto / all);
+        }
+    }
     g_last_split[0] = w.tl_steps;
     g_last_split[1] = w.blas_cur;
     g_last_split[2] = w.enters_n;
