@@ -28,6 +28,17 @@ struct alignas(16) TriRec {
 };
 static_assert(sizeof(TriRec) == 48, "TriRec is three 16-byte loads");
 
+// TriShade 128 B: what the shading of a hit on triangle t of a mesh reads
+// (path_tracer.hh:373-392: three indices, then each vertex's normal, albedo
+// and material), gathered once per mesh at tri_shade[index_offset/3 + t]:
+// vertex k's normal xyz, albedo xyz and material xyzw at floats 10k..10k+9,
+// then 2 pad floats - eight 16-byte loads of one 128-byte line instead of
+// three index loads and nine dependent gathers.
+struct alignas(16) TriShade {
+    float v[32];
+};
+static_assert(sizeof(TriShade) == 128, "TriShade is one 128-byte line");
+
 struct alignas(16) InstTrav {
     // row k = inv_transform.r[k].{x,y,z} in xyz; w = the BLAS's root block,
     // the mesh's triangle base, 0, 0 for rows 0..3: four whole, aligned
@@ -64,6 +75,7 @@ struct DevScene {
     const BlockCopy* blocks;       // block BVH records of both levels (block_format.h), 8 copies per block
     const uint32_t* tlas_root;     // per subframe: its TLAS's root block
     const TriRec* tris;
+    const TriShade* tri_shade;     // per mesh triangle, at the TriRec's index
     const InstTrav* inst_trav;
     const InstShade* inst_shade;
     const InstBox* inst_box;       // per instance: TLAS leaf box + membership (occluder candidates)

@@ -1100,6 +1100,54 @@ PTG_D f3 ld3(const float* base, uint32_t i)
 }
 PTG_D float4 ld4(const float* base, uint32_t i) { return reinterpret_cast<const float4*>(base)[i]; }
 
+// A hit triangle's vertex attributes (path_tracer.hh:373-392): normals,
+// albedos, materials of vertices indices[ioff + 3 prim + k] + bv.  The device
+// scene reads them from the triangle's TriShade line (the same values,
+// gathered once per mesh by k_pack_tris); the reference-layout scene gathers
+// them through the indices.
+struct TriAttrs {
+    f3 n[3];
+    float4 a[3], m[3];
+};
+PTG_D TriAttrs tri_attrs(const DevScene& sc, uint32_t ioff, uint32_t, uint32_t prim)
+{
+    const float4* q = reinterpret_cast<const float4*>(sc.tri_shade + ioff / 3u + prim);
+    float f[32];
+#pragma unroll
+    for(int r = 0; r < 8; ++r)
+    {
+        const float4 v = q[r];
+        f[4 * r] = v.x;
+        f[4 * r + 1] = v.y;
+        f[4 * r + 2] = v.z;
+        f[4 * r + 3] = v.w;
+    }
+    TriAttrs t;
+#pragma unroll
+    for(int k = 0; k < 3; ++k)
+    {
+        const float* g = f + 10 * k;
+        t.n[k] = V3(g[0], g[1], g[2]);
+        t.a[k] = make_float4(g[3], g[4], g[5], 0.0f);
+        t.m[k] = make_float4(g[6], g[7], g[8], g[9]);
+    }
+    return t;
+}
+PTG_D TriAttrs tri_attrs(const RefScene& sc, uint32_t ioff, uint32_t bv, uint32_t prim)
+{
+    const uint32_t tri = ioff + prim * 3;
+    const uint32_t i[3] = {sc.indices[tri] + bv, sc.indices[tri + 1] + bv, sc.indices[tri + 2] + bv};
+    TriAttrs t;
+#pragma unroll
+    for(int k = 0; k < 3; ++k)
+    {
+        t.n[k] = ld3(sc.normal, i[k]);
+        t.a[k] = ld4(sc.albedo, i[k]);
+        t.m[k] = ld4(sc.material, i[k]);
+    }
+    return t;
+}
+
 // The shading half of trace_ray (path_tracer.hh:351-411): turn the closest
 // hit of the ray (origin, dir) into a hit_info.
 // KIND: 0 = either, 1 = the caller knows the ray hit, 2 = it knows it missed
@@ -1127,11 +1175,10 @@ PTG_D HitInfo hit_info(const SC& sc, const Light& L, f3 origin, f3 dir, const Hi
     m3 rot;
     uint32_t ioff, bv;
     shade_instance(sc, h.instance_id, rot, ioff, bv);
-    const uint32_t tri = ioff + h.primitive_id * 3;
-    const uint32_t i0 = sc.indices[tri] + bv, i1 = sc.indices[tri + 1] + bv, i2 = sc.indices[tri + 2] + bv;
-    const f3 n0 = ld3(sc.normal, i0), n1 = ld3(sc.normal, i1), n2 = ld3(sc.normal, i2);
-    const float4 a0 = ld4(sc.albedo, i0), a1 = ld4(sc.albedo, i1), a2 = ld4(sc.albedo, i2);
-    const float4 m0 = ld4(sc.material, i0), m1 = ld4(sc.material, i1), m2 = ld4(sc.material, i2);
+    const TriAttrs ta = tri_attrs(sc, ioff, bv, h.primitive_id);
+    const f3 n0 = ta.n[0], n1 = ta.n[1], n2 = ta.n[2];
+    const float4 a0 = ta.a[0], a1 = ta.a[1], a2 = ta.a[2];
+    const float4 m0 = ta.m[0], m1 = ta.m[1], m2 = ta.m[2];
     const float bx = h.bx, by = h.by, bz = h.bz;
     hi.albedo = V3(a0.x * bx + a1.x * by + a2.x * bz, a0.y * bx + a1.y * by + a2.y * bz, a0.z * bx + a1.z * by + a2.z * bz);
     const float mx = m0.x * bx + m1.x * by + m2.x * bz;

@@ -1,6 +1,6 @@
 // HIP kernels + C ABI of the GPU renderer (include/ptg.h).
 //
-//   k_pack_tris     indices + positions -> TriRec (48 B / triangle)
+//   k_pack_tris     indices + positions -> TriRec (48 B / triangle), + vertex attributes -> TriShade (128 B)
 //   (BVH blocks are packed on the host, host/block_bvh.cpp)
 //   k_trace         path_trace_pixel for a (pixel set x sample chunk) grid,
 //                   one work-item per (pixel, sample); results to a
@@ -72,8 +72,12 @@ struct MeshJob {
     uint32_t index_offset, triangle_count, base_vertex_offset, pad;
 };
 
+// one thread per triangle of each new mesh: its TriRec (positions) and its
+// TriShade (normals, albedos, materials), both at index_offset / 3 + t
 __global__ void k_pack_tris(const uint32_t* __restrict__ indices, const float4* __restrict__ pos, TriRec* __restrict__ out,
-                            const MeshJob* __restrict__ jobs)
+                            const MeshJob* __restrict__ jobs, const float4* __restrict__ normal,
+                            const float4* __restrict__ albedo, const float4* __restrict__ material,
+                            TriShade* __restrict__ shade)
 {
     const MeshJob j = jobs[blockIdx.y];
     for(uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < j.triangle_count; t += gridDim.x * blockDim.x)
@@ -87,6 +91,18 @@ __global__ void k_pack_tris(const uint32_t* __restrict__ indices, const float4* 
         r.p1y = b.y; r.p1z = b.z; r.p2x = c.x; r.p2y = c.y;
         r.p2z = c.z; r.pad0 = 0; r.pad1 = 0; r.pad2 = 0;
         out[j.index_offset / 3u + t] = r;
+        TriShade sh;
+        for(int k = 0; k < 3; ++k)
+        {
+            const uint32_t v = j.base_vertex_offset + tri[k];
+            const float4 n = normal[v], a = albedo[v], m = material[v];
+            float* g = sh.v + 10 * k;
+            g[0] = n.x; g[1] = n.y; g[2] = n.z;
+            g[3] = a.x; g[4] = a.y; g[5] = a.z;
+            g[6] = m.x; g[7] = m.y; g[8] = m.z; g[9] = m.w;
+        }
+        sh.v[30] = sh.v[31] = 0.0f;
+        shade[j.index_offset / 3u + t] = sh;
     }
 }
 
@@ -841,7 +857,7 @@ struct ptg_context {
     // static scene: the shading arrays in reference layout, the triangle
     // records, and a host copy of the BLAS nodes + links (packed into blocks
     // when an instance first names a BLAS)
-    DevBuf indices, pos, normal, albedo, material, tris;
+    DevBuf indices, pos, normal, albedo, material, tris, tri_shade;
     std::vector<ptg_bvh_node> host_nodes;
     std::vector<ptg_bvh_link> host_links;
     std::vector<uint32_t> host_indices;    // the mesh arrays the occluder candidates' leaf boxes are checked against
@@ -967,6 +983,7 @@ struct ptg_context {
         s.blocks = blocks.as<BlockCopy>();
         s.tlas_root = tlas_root.as<uint32_t>();
         s.tris = tris.as<TriRec>();
+        s.tri_shade = tri_shade.as<TriShade>();
         s.inst_trav = inst_trav.as<InstTrav>();
         s.inst_shade = inst_shade.as<InstShade>();
         s.inst_box = inst_box.as<InstBox>();
@@ -1408,6 +1425,9 @@ int ptg_context_create(int device, ptg_context** out)
     // grid-stride kernels (camera, classify, shade, sky): 32 blocks per CU,
     // measured best of 3..128
     ctx->persistent_blocks = uint32_t(std::max(1, prop.multiProcessorCount)) * 32u;
+    // timing knobs: chunk size and HBM share of a renderer that owns the GPU
+    ctx->chunk_log2 = std::min<uint32_t>(28u, std::max<uint32_t>(16u, env_knob("PTG_CHUNK_LOG2", ctx->chunk_log2)));
+    ctx->hbm_pct = std::min<uint32_t>(70u, std::max<uint32_t>(5u, env_knob("PTG_HBM_SHARE", ctx->hbm_pct)));
     // Walk residency: each walk lane holds its world ray (32 B) and its stack
     // window (8 x kCap B) in LDS, so the walk blocks' LDS sets how many are
     // resident per CU: kWalkResident (the LDS is padded to that share).
@@ -1531,6 +1551,7 @@ int ptg_upload_scene(ptg_context* ctx, const ptg_bvh_node* nodes, const ptg_bvh_
     // slack: the walk's leaf phase reads a triangle as four 16-byte rows (the
     // 48-byte record and the next 16 bytes)
     PTG_HIP(ctx->tris.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriRec) + 128));
+    PTG_HIP(ctx->tri_shade.reserve(std::max<size_t>(1, index_count / 3) * sizeof(TriShade)));
     hipStream_t s = ctx->stream;
     PTG_HIP(hipMemcpyAsync(ctx->indices.p, indices, index_count * 4, hipMemcpyHostToDevice, s));
     PTG_HIP(hipMemcpyAsync(ctx->pos.p, pos, vertex_count * 16, hipMemcpyHostToDevice, s));
@@ -1729,7 +1750,8 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
         for(const MeshJob& j: mesh_jobs) maxt = std::max(maxt, j.triangle_count);
         dim3 grid(std::min<uint32_t>(grid_for(maxt), 4096), uint32_t(mesh_jobs.size()));
         hipLaunchKernelGGL(k_pack_tris, grid, dim3(kBlock), 0, s, ctx->indices.as<uint32_t>(), ctx->pos.as<float4>(),
-                           ctx->tris.as<TriRec>(), ctx->jobs.as<MeshJob>());
+                           ctx->tris.as<TriRec>(), ctx->jobs.as<MeshJob>(), ctx->normal.as<float4>(),
+                           ctx->albedo.as<float4>(), ctx->material.as<float4>(), ctx->tri_shade.as<TriShade>());
         PTG_HIP(hipGetLastError());
     }
 
