@@ -142,6 +142,7 @@ struct RegCold {
     PTG_D uint32_t candidate_root() const { return kBePop; }
     PTG_D void set_candidate(uint32_t, uint32_t) {}
     PTG_D void clear_candidate_root() {}
+    static constexpr bool kGlobalTri = false;   // confirm() takes the mesh-local primitive
     // ray_query_confirm (ray_query.hh:280-290)
     PTG_D void confirm(float u, float v, float t, uint32_t instance, uint32_t prim, bool back)
     {
@@ -198,6 +199,9 @@ struct LdsCold {
         typedef __attribute__((address_space(3))) float lds_f_t;
         reinterpret_cast<lds_f_t*>(c)[7] = __uint_as_float(kBePop);
     }
+    // confirm() takes the BLAS's triangle base + the primitive (the TriRec /
+    // TriShade index), which the wavefront hit record carries to the shading
+    static constexpr bool kGlobalTri = true;
     PTG_D f3 world_o() const { const lds_f4v v = c[0]; return V3(v.x, v.y, v.z); }
     PTG_D f3 world_d() const { const lds_f4v v = c[1]; return V3(v.x, v.y, v.z); }
     // ray_query_confirm (ray_query.hh:280-290); thit is the walk's tmax, bz is
@@ -635,7 +639,7 @@ struct BlockWalker {
                 cur = leaf;   // the occluder, for the caller (the walk has ended)
                 return 2;
             }
-            cold.confirm(u, v, t, inst, leaf, back);
+            cold.confirm(u, v, t, inst, Cold::kGlobalTri ? tri_base + leaf : leaf, back);
             tmax = t;
         }
         return 0;
@@ -1109,9 +1113,9 @@ struct TriAttrs {
     f3 n[3];
     float4 a[3], m[3];
 };
-PTG_D TriAttrs tri_attrs(const DevScene& sc, uint32_t ioff, uint32_t, uint32_t prim)
+PTG_D TriAttrs tri_attrs_at(const DevScene& sc, uint32_t tri)
 {
-    const float4* q = reinterpret_cast<const float4*>(sc.tri_shade + ioff / 3u + prim);
+    const float4* q = reinterpret_cast<const float4*>(sc.tri_shade + tri);
     float f[32];
 #pragma unroll
     for(int r = 0; r < 8; ++r)
@@ -1133,7 +1137,14 @@ PTG_D TriAttrs tri_attrs(const DevScene& sc, uint32_t ioff, uint32_t, uint32_t p
     }
     return t;
 }
-PTG_D TriAttrs tri_attrs(const RefScene& sc, uint32_t ioff, uint32_t bv, uint32_t prim)
+// KIND 1 (the wavefront's surface pass): `prim` is the walk's mesh-global
+// triangle (LdsCold::kGlobalTri), so the attribute line's address does not
+// wait for the instance record
+template<int KIND> PTG_D TriAttrs tri_attrs(const DevScene& sc, uint32_t ioff, uint32_t, uint32_t prim)
+{
+    return tri_attrs_at(sc, KIND == 1 ? prim : ioff / 3u + prim);
+}
+template<int KIND> PTG_D TriAttrs tri_attrs(const RefScene& sc, uint32_t ioff, uint32_t bv, uint32_t prim)
 {
     const uint32_t tri = ioff + prim * 3;
     const uint32_t i[3] = {sc.indices[tri] + bv, sc.indices[tri + 1] + bv, sc.indices[tri + 2] + bv};
@@ -1175,7 +1186,7 @@ PTG_D HitInfo hit_info(const SC& sc, const Light& L, f3 origin, f3 dir, const Hi
     m3 rot;
     uint32_t ioff, bv;
     shade_instance(sc, h.instance_id, rot, ioff, bv);
-    const TriAttrs ta = tri_attrs(sc, ioff, bv, h.primitive_id);
+    const TriAttrs ta = tri_attrs<KIND>(sc, ioff, bv, h.primitive_id);
     const f3 n0 = ta.n[0], n1 = ta.n[1], n2 = ta.n[2];
     const float4 a0 = ta.a[0], a1 = ta.a[1], a2 = ta.a[2];
     const float4 m0 = ta.m[0], m1 = ta.m[1], m2 = ta.m[2];

@@ -41,7 +41,7 @@ struct PathSoA {
 
 // Per-queue-position results of the trace kernels.
 struct TraceOut {
-    uint4* hit;       // thit bits, instance, primitive, back_face
+    uint4* hit;       // thit bits, instance, mesh-global triangle (BLAS triangle base + primitive), back_face
     float4* bary;     // barycentrics
     uint32_t* shadow; // 1 = the pending NEE ray is occluded
 };

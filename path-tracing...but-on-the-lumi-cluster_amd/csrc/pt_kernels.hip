@@ -339,6 +339,7 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
         else
         {
             const Hit h = w.result();
+            // (primitive_id: the mesh-global triangle, LdsCold::kGlobalTri)
             nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
             if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
                 nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
