@@ -160,16 +160,16 @@ class Reference:
             raise RuntimeError("ref_pt %s failed (%d): %s" % (args, r.returncode, r.stderr[-2000:]))
         return r.stdout
 
-    def samples(self, assets, frame, x0, y0, w, h, j0, j1):
+    def samples(self, assets, frame, x0, y0, w, h, j0, j1, timeout=3600):
         with tempfile.TemporaryDirectory() as d:
             p = os.path.join(d, "s.f32")
-            self.run(assets, "samples", frame, x0, y0, w, h, j0, j1, p)
+            self.run(assets, "samples", frame, x0, y0, w, h, j0, j1, p, timeout=timeout)
             return np.fromfile(p, np.float32).reshape(h, w, j1 - j0, 4)
 
-    def render(self, assets, frame):
+    def render(self, assets, frame, timeout=3600):
         with tempfile.TemporaryDirectory() as d:
             p = os.path.join(d, "r")
-            self.run(assets, "render", frame, p)
+            self.run(assets, "render", frame, p, timeout=timeout)
             acc = np.fromfile(p + ".f32", np.float32).reshape(self.h, self.w, 4)
             bgra = np.fromfile(p + ".bgra", np.uint8).reshape(self.h, self.w, 4)
             return acc, bgra
