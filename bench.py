@@ -347,6 +347,10 @@ def main():
     ap.add_argument("--tile", type=str, default="32x16")
     ap.add_argument("--concurrency", type=int, default=2, choices=[0, 1, 2],
                     help="ptg_set_concurrency level of the timed steps (profiling passes use 0)")
+    ap.add_argument("--gpu-memory", choices=["owned", "shared"], default="owned",
+                    help="owned (default: the bench process owns its GPU): 2^28-path sample chunks, <= 40%% of HBM "
+                         "per chunk pipeline (ptg_set_chunk_paths / ptg_set_hbm_share); shared: the library's "
+                         "defaults (2^27, 35%%), which leave most of the GPU to other tenants.  Same bits either way")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
@@ -430,6 +434,9 @@ def main():
     stream = torch.cuda.current_stream(local)
     r.set_stream(stream)
     r.set_concurrency(args.concurrency)
+    if args.gpu_memory == "owned":
+        r.set_hbm_share(40)
+        r.set_chunk_paths(28)
     tw, th = [int(v) for v in args.tile.split("x")]
     frame = args.frame + (rank if args.shard == "frames" else 0)
 
@@ -799,7 +806,10 @@ def main():
             "data": "synthetic: reference scene assets + deterministic substitutes, frame %d" % args.frame,
             "config": {"workload": workload + (" (BASELINE metric config)" if is_metric else ""),
                        "baseline_config": args.config,
-                       "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world)},
+                       "shard": args.shard, "parallelism": "%s x%d" % (args.shard, world),
+                       "gpu_memory": ("owned: sample chunks of <= 2^28 paths, <= 40% of HBM per chunk pipeline"
+                                      if args.gpu_memory == "owned" else
+                                      "shared: the library's defaults, <= 2^27 paths and 35% of HBM per pipeline")},
             "frame_exact": None if main_check is None else main_check["exact"],
             "frame_check": main_check,
             "selftest": selftest,

@@ -326,6 +326,12 @@ int ptg_set_concurrency(ptg_context* ctx, int level);
  * the bits do not change. */
 int ptg_set_hbm_share(ptg_context* ctx, int percent);
 
+/* Live paths per sample chunk and pipeline: at most 2^log2_paths (16-28,
+ * default 27: ~53 GB of path state per pipeline).  A renderer that owns the
+ * GPU takes 28 with a 40% HBM share (4 chunks of 256 spp at 1280x720x1024,
+ * ~74% of HBM); the bits do not change. */
+int ptg_set_chunk_paths(ptg_context* ctx, int log2_paths);
+
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);
 

@@ -42,7 +42,7 @@ struct PathSoA {
 // Per-queue-position results of the trace kernels.
 struct TraceOut {
     uint4* hit;       // thit bits, instance, mesh-global triangle (BLAS triangle base + primitive), back_face
-    float4* bary;     // barycentrics
+    float2* bary;     // barycentrics u, v (w = 1 - u - v is recomputed)
     uint32_t* shadow; // 1 = the pending NEE ray is occluded
 };
 

@@ -264,8 +264,8 @@ constexpr uint32_t kBands = 1024;   // XCD bands of a walk queue: a multiple of 
 constexpr uint32_t kCountWords(uint32_t rounds) { return 4 * (rounds + 2) + 2 * rounds; }
 // a chunk pipeline's state bytes per queued path, as render_map carves them:
 // 2 ping-pong PathSoA halves of 9 x 16 B, 2 TraceOut sets (hit 16 B, bary
-// 16 B, shadow 4 B), 5 lists of 4 B (2 NEE lists, hit, sky, redo)
-constexpr size_t kStateBytesPerPath = 2 * 9 * 16 + 2 * (16 + 16 + 4) + 5 * 4;
+// 8 B, shadow 4 B), 5 lists of 4 B (2 NEE lists, hit, sky, redo)
+constexpr size_t kStateBytesPerPath = 2 * 9 * 16 + 2 * (16 + 8 + 4) + 5 * 4;
 constexpr uint32_t kRedoGrid = 16;   // blocks of the MathExact shading passes (grid-stride over a short list)
 
 // Walk statistics of the counting build (per walk kind, see WalkStats): how
@@ -342,7 +342,8 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
             // (primitive_id: the mesh-global triangle, LdsCold::kGlobalTri)
             nt_store(tr.hit + q, make_uint4(__float_as_uint(h.thit), h.instance_id, h.primitive_id, h.back_face ? 1u : 0u));
             if(h.instance_id != 0xFFFFFFFFu)   // a miss is shaded without its barycentrics
-                nt_store(tr.bary + q, make_float4(h.bx, h.by, h.bz, 0.f));
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, make_float2(h.bx, h.by)),
+                                            reinterpret_cast<unsigned long long*>(tr.bary + q));
         }
     };
     unsigned long long ws[WS_COUNT] = {};   // COUNT: lane 0's tallies for its wave
@@ -539,12 +540,13 @@ __device__ __forceinline__ void load_queued(const PathSoA& cur, const TraceOut& 
         return;
     }
     const uint4 hv = ld_state(tr.hit + q);
-    const float4 bv = ld_state(tr.bary + q);
+    // (bz = 1 - bx - by, the same float arithmetic as the walk's result())
+    const float2 bv = __builtin_bit_cast(float2, __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(tr.bary + q)));
     h.thit = __uint_as_float(hv.x);
     h.instance_id = hv.y;
     h.primitive_id = hv.z;
     h.back_face = hv.w != 0;
-    h.bx = bv.x; h.by = bv.y; h.bz = bv.z;
+    h.bx = bv.x; h.by = bv.y; h.bz = 1.0f - bv.x - bv.y;
 }
 
 // A shading kernel's math policy (ref_math.h); MathExactLds copies glibc
@@ -1147,7 +1149,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
             for(TraceOut& o: t.trs)
             {
                 o.hit = reinterpret_cast<uint4*>(b); b += M * 16;
-                o.bary = reinterpret_cast<float4*>(b); b += M * 16;
+                o.bary = reinterpret_cast<float2*>(b); b += M * 8;
                 o.shadow = reinterpret_cast<uint32_t*>(b); b += M * 4;
             }
             t.lists[0] = reinterpret_cast<uint32_t*>(b); b += M * 4;
@@ -2073,6 +2075,13 @@ int ptg_set_hbm_share(ptg_context* ctx, int percent)
 {
     if(!ctx || percent < 5 || percent > 70) return fail(PTG_E_INVALID, "ptg_set_hbm_share: 5 .. 70 percent");
     ctx->hbm_pct = uint32_t(percent);
+    return PTG_OK;
+}
+
+int ptg_set_chunk_paths(ptg_context* ctx, int log2_paths)
+{
+    if(!ctx || log2_paths < 16 || log2_paths > 28) return fail(PTG_E_INVALID, "ptg_set_chunk_paths: 16 .. 28");
+    ctx->chunk_log2 = uint32_t(log2_paths);
     return PTG_OK;
 }
 

@@ -125,6 +125,7 @@ def lib():
         "ptg_last_walk_stats": (I, [P, P]),
         "ptg_last_redo_stats": (I, [P, P]),
         "ptg_set_hbm_share": (I, [P, I]),
+        "ptg_set_chunk_paths": (I, [P, I]),
         "ptg_set_pipeline": (I, [P, I]),
         "ptg_set_concurrency": (I, [P, I]),
         "ptg_synchronize": (I, [P]),

@@ -198,6 +198,11 @@ class GpuRenderer:
         (default 35); identical bits at any share."""
         N.check(N.lib().ptg_set_hbm_share(self._ctx, int(percent)), "ptg_set_hbm_share")
 
+    def set_chunk_paths(self, log2_paths):
+        """At most 2^log2_paths live paths per sample chunk and pipeline
+        (16-28, default 27); identical bits at any size."""
+        N.check(N.lib().ptg_set_chunk_paths(self._ctx, int(log2_paths)), "ptg_set_chunk_paths")
+
     def set_pipeline(self, name):
         """'wavefront' (default) or 'megakernel' - bit-identical results."""
         N.check(N.lib().ptg_set_pipeline(self._ctx, {"wavefront": 0, "megakernel": 1}[name]), "ptg_set_pipeline")

@@ -5,6 +5,7 @@
     buffers that must grow for a new BLAS), bit-identical to synchronised
     renders of the same frames;
   * ptg_set_hbm_share: smaller path-state chunks, identical bits;
+  * ptg_set_chunk_paths: larger or smaller sample chunks, identical bits;
   * the counting build's walk statistics (ptg_last_walk_stats) against the
     work counters of the same render;
   * two processes on one GPU, each a real GpuRenderer, rendering their tile
@@ -91,6 +92,34 @@ def test_hbm_share_changes_chunks_not_bits(assets_dir):
     assert np.array_equal(out[0][0], out[1][0])
     with pytest.raises(N.PtgError, match=r"\(-1\)"):
         GpuRenderer(0).set_hbm_share(2)
+
+
+def test_chunk_paths_change_chunks_not_bits(assets_dir):
+    """ptg_set_chunk_paths: the 1280x720 x 256 spp frame (236 M paths) in
+    chunks of at most 2^28 paths with a 40% share (what a renderer that owns
+    the GPU takes, bench.py's default) and of at most 2^24 paths: more
+    chunks for the smaller size, the same bits."""
+    from ptlumi.renderer import GpuRenderer
+    s = scene_for(assets_dir, 1280, 720, 256, frame=0)
+    arr = arrays_copy(s)
+    out = []
+    for log2, share in ((28, 40), (24, 35)):
+        r = GpuRenderer(0)
+        try:
+            r.set_hbm_share(share)
+            r.set_chunk_paths(log2)
+            r.upload_arrays(arr)
+            r.enable_timing(True)
+            _, acc = r.render(s.cfg, want_accum=True)
+            r.synchronize()
+            launches = r.kernel_times()["camera"][1]      # one camera launch per chunk
+            out.append((_bits(acc.cpu().numpy()[..., :3]), launches))
+        finally:
+            r.close()
+    assert out[1][1] > out[0][1], "smaller chunks must mean more of them: %s" % [o[1] for o in out]
+    assert np.array_equal(out[0][0], out[1][0])
+    with pytest.raises(N.PtgError, match=r"\(-1\)"):
+        GpuRenderer(0).set_chunk_paths(29)
 
 
 def test_walk_stats_consistent_with_counters(gpu, assets_dir):

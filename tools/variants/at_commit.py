@@ -21,7 +21,8 @@ open(os.path.join(sys.argv[1], ".rebuild_host"), "w").write(rev + "\n")
 p = os.path.join(sys.argv[1], "pt_kernels.hip")
 s = open(p).read()
 stubs = {"ptg_arith_selftest": 'extern "C" int ptg_arith_selftest(ptg_context*) { return -1; }   /* not available: never a passing self-test */',
-         "ptg_tonemap_device": 'extern "C" int ptg_tonemap_device(ptg_context*, size_t, const ptg_float4*, ptg_uchar4*) { return -1; }'}
+         "ptg_tonemap_device": 'extern "C" int ptg_tonemap_device(ptg_context*, size_t, const ptg_float4*, ptg_uchar4*) { return -1; }',
+         "ptg_set_chunk_paths": 'extern "C" int ptg_set_chunk_paths(ptg_context*, int) { return -1; }   /* not available */'}
 for name, body in stubs.items():
     if name not in s:
         s += "\n" + body + "\n"
