@@ -434,6 +434,11 @@ def main():
     stream = torch.cuda.current_stream(local)
     r.set_stream(stream)
     r.set_concurrency(args.concurrency)
+    # a GPU shared by several local ranks (PTG_BENCH_REHEARSE) is not owned:
+    # the library's shared defaults then (each rank's 74% would not fit)
+    shares_gpu = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(1, torch.cuda.device_count())
+    if args.gpu_memory == "owned" and shares_gpu:
+        args.gpu_memory = "shared"
     if args.gpu_memory == "owned":
         r.set_hbm_share(40)
         r.set_chunk_paths(28)
