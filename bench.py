@@ -9,7 +9,10 @@ TESTING preset), the reference scene (reference OBJ assets + committed
 substitutes for the three missing meshes).  One step = one baseline_render of
 the frame on the GPU (+ the RCCL framebuffer gather in --shard tiles mode)
 with the scene and the frame's TLAS/instances/subframes already resident in
-HBM: `value`.
+HBM: `value`.  The bench process owns its GPU (--gpu-memory owned, the
+default): sample chunks of up to 2^28 paths with 40% of HBM per chunk
+pipeline (ptg_set_chunk_paths / ptg_set_hbm_share); --gpu-memory shared keeps
+the library's defaults for a shared GPU; the bits are the same.
 
 Beside `value` the line carries (rank 0):
   with_frame_setup  what main.cc does per frame - setup_animation_frame (host
