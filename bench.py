@@ -333,6 +333,38 @@ def check_spots(spots_npz, cfg):
     return "%d/%d" % (ok, n)
 
 
+def launcher_command(n, argv, port):
+    """The child command bench.py runs for `--gpus n > 1` when no launcher
+    started it: one process per GPU under torch.distributed.run on this node,
+    rendezvous on 127.0.0.1, each rank given the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def world_check(gpus, env):
+    """None when this process may run as one rank of `gpus`; "launch" when
+    --gpus > 1 and no launcher set WORLD_SIZE (bench.py starts the ranks
+    itself); an error message when the launcher's WORLD_SIZE is not --gpus
+    (a silent N=1 line under --gpus N would be a false measurement)."""
+    w = env.get("WORLD_SIZE")
+    if w is None:
+        return "launch" if gpus > 1 else None
+    try:
+        w = int(w)
+    except ValueError:
+        return "WORLD_SIZE %r is not an integer" % w
+    if w != gpus:
+        return "--gpus %d but WORLD_SIZE %d: refusing to report a %d-rank run as %d GPUs" % (gpus, w, w, gpus)
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -372,6 +404,18 @@ def main():
     ap.add_argument("--spots-out", default=None,
                     help="npz of every animation frame's spot rectangles (default gpurun_out/anim_spots_r<rank>.npz)")
     args = ap.parse_args()
+    # N > 1 without a launcher: start N ranks as a child process (before this
+    # process imports torch or touches a GPU) and forward its output and exit
+    # code; a launcher whose world size is not --gpus is an error, not a warning
+    wc = world_check(args.gpus, os.environ)
+    if wc == "launch":
+        import subprocess
+        cmd = launcher_command(args.gpus, sys.argv[1:], free_port())
+        print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+        sys.exit(subprocess.call(cmd))
+    if wc is not None:
+        print("bench.py: %s" % wc, file=sys.stderr, flush=True)
+        sys.exit(2)
     if args.config == 1:
         args.width, args.height, args.spp, args.frame = 1280, 720, 256, 0
     elif args.config == 2:
@@ -397,8 +441,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     # PTG_BENCH_REHEARSE=1: rehearse the N>1 code paths with more ranks than GPUs
     # (ranks share devices, gloo instead of RCCL, which cannot put two ranks on
     # one GPU); never used for a measurement
@@ -444,7 +486,10 @@ def main():
         args.gpu_memory = "shared"
     if args.gpu_memory == "owned":
         r.set_hbm_share(40)
-        r.set_chunk_paths(28)
+        try:
+            r.set_chunk_paths(28)
+        except N.PtgError:   # a timing build of older sources without ptg_set_chunk_paths
+            args.gpu_memory = "shared (2^28-path chunks unavailable)"
     tw, th = [int(v) for v in args.tile.split("x")]
     frame = args.frame + (rank if args.shard == "frames" else 0)
 
@@ -689,6 +734,32 @@ def main():
     value_upload = samples_per_step * args.steps / elapsed_upload / 1e6 if elapsed_upload else None
     value_frame = samples_per_step * args.steps / elapsed_frame / 1e6 if elapsed_frame else None
 
+    # (3b) N > 1 under the default frame shard: the strong-scaling companion,
+    # the metric frame itself cut into interleaved tiles over the same ranks
+    # and assembled on rank 0 by one RCCL gather (BASELINE configs[2])
+    strong = None
+    if world > 1 and args.shard == "frames":
+        scene.setup_frame(args.frame)
+        r.upload(scene, include_static=False)
+        tshard = D.TileShard(cfg, tw, th, rank, world)
+        full = torch.zeros_like(image)
+
+        def strong_step():
+            D.render_and_gather(r, cfg, tshard, full, stream=stream)
+
+        el_s, _ = timed(strong_step, False, tag="strong_tiles")
+        strong = {"value": round(cfg.width * cfg.height * cfg.samples_per_pixel * args.steps / el_s / 1e6, 3),
+                  "unit": "Msamples/s", "ms_per_step": round(el_s / args.steps * 1e3, 3), "steps": args.steps,
+                  "scaling": "strong", "frame": args.frame, "shard": "tiles %dx%d round-robin over %d ranks" % (tw, th, world),
+                  "step": "render this rank's tiles + one gather of the BGRA tiles to rank 0 + scatter into the "
+                          "framebuffer (distributed.render_and_gather)"}
+        if rank == 0:
+            want = frame_golden(cfg, args.frame)
+            if want is not None:
+                import hashlib
+                got = hashlib.sha256(np.ascontiguousarray(full.cpu().numpy()).tobytes()).hexdigest()[:32]
+                strong["bgra_exact"] = got == want["sha_bgra"]
+
     # (3) the heavy companion frame at the same configuration, with its own roofline
     heavy = None
     if args.heavy_frame >= 0:
@@ -824,6 +895,7 @@ def main():
             "libm": libm_identity(),
             "ranks": ranks,
             "per_rank_seconds": {k: [round(x, 4) for x in v] for k, v in per_rank_s.items()} if world > 1 else None,
+            "strong": strong,
             "heavy_frame": heavy,
             "animation": anim,
             "value_survey_def": None if value_upload is None else {
@@ -846,6 +918,25 @@ def main():
                 result["gpu_vs_cpu_socket_estimate"] = [round(value / hi, 2), round(value / lo, 2)]
             if heavy and cpu.get("heavy_frame"):
                 result["heavy_gpu_vs_cpu"] = round(heavy["value"] / cpu["heavy_frame"]["value"], 2)
+        # the evidence a reader of the line's tail needs, last and flat (the
+        # driver keeps only the last ~2000 characters of stdout)
+        result["summary"] = {
+            "value": result["value"], "n_gpus": result["n_gpus"], "ms_per_step": result["ms_per_step"],
+            "frame_exact": result["frame_exact"],
+            "heavy_ms": heavy["ms_per_step"] if heavy else None,
+            "heavy_value": heavy["value"] if heavy else None,
+            "heavy_frame_exact": (heavy.get("frame_check") or {}).get("exact") if heavy else None,
+            "anim_frames_per_min": anim["frames_per_min"] if anim else None,
+            "anim_spots": anim["spots_exact"] if anim else None,
+            "strong_value": strong["value"] if strong else None,
+            "strong_bgra_exact": strong.get("bgra_exact") if strong else None,
+            "distinct_gpus": ranks["distinct_gpus"] if ranks else 1,
+            "roofline_frac": roof.get("frac") if roof else None,
+            "roofline_bound": roof.get("bound") if roof else None,
+            "heavy_roofline_frac": ((heavy or {}).get("roofline") or {}).get("frac"),
+            "cpu_value": cpu.get("value") if cpu else None,
+            "gpu_vs_cpu": result.get("gpu_vs_cpu"),
+            "selftest": selftest}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -158,6 +158,12 @@ void ptg_context_destroy(ptg_context* ctx);
  * already queued on the previous stream is ordered before anything queued on
  * the new one (an event recorded there, waited on by the new stream). */
 int ptg_context_set_stream(ptg_context* ctx, void* hip_stream);
+/* The hipStream_t the context launches on (*out; NULL = the legacy default
+ * stream), so a caller can order its own work - e.g. an RCCL collective over
+ * the rendered tiles (include/ptg_rccl.h) - after the context's. */
+int ptg_context_get_stream(ptg_context* ctx, void** out);
+/* The HIP device ordinal of the context (*out). */
+int ptg_context_device(ptg_context* ctx, int* out);
 
 /* Once per run: the static part of the arrays (everything load_scene
  * produced).  nodes/links hold node_count BVH nodes (links: 8 per node, the
@@ -327,10 +333,22 @@ int ptg_set_concurrency(ptg_context* ctx, int level);
 int ptg_set_hbm_share(ptg_context* ctx, int percent);
 
 /* Live paths per sample chunk and pipeline: at most 2^log2_paths (16-28,
- * default 27: ~53 GB of path state per pipeline).  A renderer that owns the
- * GPU takes 28 with a 40% HBM share (4 chunks of 256 spp at 1280x720x1024,
- * ~74% of HBM); the bits do not change. */
+ * default 27: 2^27 x 380 B = ~51 GB of path state per pipeline).  A renderer
+ * that owns the GPU takes 28 with a 40% HBM share (4 chunks of 256 spp at
+ * 1280x720x1024, ~71% of HBM); the bits do not change. */
 int ptg_set_chunk_paths(ptg_context* ctx, int log2_paths);
+
+/* Environment knobs read once by ptg_context_create (timing experiments;
+ * no result bit depends on any of them; a malformed or out-of-range value is
+ * ignored).  An embedding application that must not have its memory use or
+ * launch shape changed from outside should leave them unset:
+ *   PTG_CHUNK_LOG2              initial ptg_set_chunk_paths value (16-28)
+ *   PTG_HBM_SHARE               initial ptg_set_hbm_share value (5-70)
+ *   PTG_WALK_RESIDENT[_ANY]     closest-hit [any-hit] walk blocks resident per
+ *                               CU (pads the blocks' LDS; 0-64)
+ *   PTG_WALK_BLOCKS[_ANY]       closest-hit [any-hit] walk blocks launched per
+ *                               CU (0-64)
+ * The ptg_set_* calls after ptg_context_create override the first two. */
 
 /* Synchronise the context's stream. */
 int ptg_synchronize(ptg_context* ctx);

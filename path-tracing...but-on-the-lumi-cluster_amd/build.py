@@ -27,7 +27,8 @@ REF_CONFIGS = [
     ("v3", 1280, 720, 16, 4),        # CPU baseline (reference flags, portable -march)
     ("v3", 640, 360, 32, 4),         # CPU baseline configs[0] (one core); strict-vs-shipped statistics
 ]
-# reference host code + ptg_render in place of baseline_render (oracle/dropin_main.cc)
+# reference host code + ptg_render in place of baseline_render (oracle/dropin_main.cc),
+# and + ptg_render_gather over an RCCL communicator (oracle/dropin_rccl.cc)
 DROPIN_CONFIGS = [("strict", 160, 90, 32, 4)]
 
 
@@ -55,8 +56,8 @@ def build_oracle(verbose=False, jobs=8, with_reference=None):
             _run(["make", "-j%d" % jobs, "ref", "REF_MODE=%s" % mode, "REF_W=%d" % w, "REF_H=%d" % h,
                   "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
         for mode, w, h, spp, b in DROPIN_CONFIGS:   # needs libptg.so: build_native first
-            _run(["make", "-j%d" % jobs, "dropin", "REF_MODE=%s" % mode, "REF_W=%d" % w, "REF_H=%d" % h,
-                  "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
+            _run(["make", "-j%d" % jobs, "dropin", "dropin_rccl", "REF_MODE=%s" % mode, "REF_W=%d" % w,
+                  "REF_H=%d" % h, "REF_SPP=%d" % spp, "REF_BOUNCES=%d" % b], ORACLE, verbose)
 
 
 def build_test_kernels(verbose=False):

@@ -1644,6 +1644,10 @@ PTG_D bool nee_term_moot(f3 att, f3 contrib, const NeeCandidate& c)
     const uint32_t az = (__float_as_uint(att.x) | __float_as_uint(att.y) | __float_as_uint(att.z)) & 0x7FFFFFFFu;
     if(az != 0u) return false;
     if(!finite3(c.color) || !(c.mis_pdf > 0.0f) || !__builtin_isfinite(c.mis_pdf)) return false;
+    // (colour * A) / mis_pdf with A in [+0, 1] is at most colour / mis_pdf in
+    // magnitude (rounding is monotone): finite when that is (a colour near
+    // FLT_MAX from ptg_upload_frame could otherwise overflow to inf)
+    if(!finite3(c.color / c.mis_pdf)) return false;
     const bool neg0x = __float_as_uint(contrib.x) == 0x80000000u && (__float_as_uint(c.color.x) >> 31);
     const bool neg0y = __float_as_uint(contrib.y) == 0x80000000u && (__float_as_uint(c.color.y) >> 31);
     const bool neg0z = __float_as_uint(contrib.z) == 0x80000000u && (__float_as_uint(c.color.z) >> 31);
@@ -1661,10 +1665,26 @@ PTG_D bool nee_term_moot(f3 att, f3 contrib, const NeeCandidate& c)
 // see bounce_tail) and mis_pdf neither 0 nor NaN for the hit and for both
 // miss cases (nee_pdf 0 or the sun disk's, hit_info), both terms are +-0;
 // and x + (+-0) == x bitwise for every x but -0, which contrib must not hold.
+// The sky's terms of a retiring path - the sun-disk albedo (visible * colour)
+// * w with w the disk's pdf 1 / (2 pi (1 - cos)), and the in-scatter, the
+// colour times the atmosphere's bounded integrals (at most ~1e3 over the 8 x 4
+// steps, nishita_atmosphere_scattering) - are finite when the colour is finite
+// and its magnitude times max(w, 1) stays below 2^100 (2^28 of headroom).  The
+// zero-throughput shortcuts need X finite; a light from ptg_upload_frame is
+// not validated, so a NaN, infinite or huge colour, or a degenerate cone,
+// takes the full computation.
+PTG_D bool sky_terms_finite(const Light& L)
+{
+    const float sun = 1.0f / (2.0f * PI_F * (1.0f - L.cos));
+    if(!finite3(L.color) || !__builtin_isfinite(sun)) return false;
+    const float m = gmax(fabsf(L.color.x), gmax(fabsf(L.color.y), fabsf(L.color.z))) * gmax(fabsf(sun), 1.0f);
+    return m < 0x1p100f;
+}
+
 PTG_D bool last_bounce_moot(f3 att, f3 batt, float bpdf, f3 contrib, const Light& L)
 {
     const uint32_t az = (__float_as_uint(att.x) | __float_as_uint(att.y) | __float_as_uint(att.z)) & 0x7FFFFFFFu;
-    if(az != 0u || !finite3(batt) || !finite3(L.color)) return false;
+    if(az != 0u || !finite3(batt) || !sky_terms_finite(L)) return false;
     if(__float_as_uint(contrib.x) == 0x80000000u || __float_as_uint(contrib.y) == 0x80000000u ||
        __float_as_uint(contrib.z) == 0x80000000u)
         return false;
@@ -1784,7 +1804,7 @@ PTG_D void bounce_tail(u4& seed, const Light& L, f3 ray_o, f3 ray_dir, HitInfo& 
                              __float_as_uint(attenuation.z)) & 0x7FFFFFFFu;
         const uint32_t colour_signs = (__float_as_uint(L.color.x) | __float_as_uint(L.color.y) |
                                        __float_as_uint(L.color.z)) >> 31;
-        if(az == 0u && colour_signs == 0u && __builtin_isfinite(mis_pdf) && mis_pdf != 0.0f)
+        if(az == 0u && colour_signs == 0u && __builtin_isfinite(mis_pdf) && mis_pdf != 0.0f && sky_terms_finite(L))
         {
             contribution = contribution + (attenuation * V3(0.0f, 0.0f, 0.0f)) / mis_pdf;
             return;

@@ -901,10 +901,10 @@ struct ptg_context {
     uint32_t walk_xcds[2] = {1, 1};        // XCDs the walk grid is dealt over (8 when the grid divides evenly)
     uint32_t walk_lds[2] = {0, 0};         // dynamic LDS per walk block: cold state + stack rings, padded to cap residency
     uint32_t hbm_pct = 35;                 // wavefront state: at most this share of HBM per chunk pipeline (ptg_set_hbm_share)
-    // wavefront: <= 2^chunk_log2 live paths per chunk.  2^27 paths x 396 B
-    // (kStateBytesPerPath + the 16 B sample) = 53 GB per pipeline, ~37% of an MI355X's HBM for the two pipelines
+    // wavefront: <= 2^chunk_log2 live paths per chunk.  2^27 paths x 380 B
+    // (kStateBytesPerPath 364 + the 16 B sample) = 51 GB per pipeline, ~35% of an MI355X's HBM for the two pipelines
     // together, so a default render leaves most of the GPU to other tenants;
-    // 2^28 (73%) is 1-3% faster on a GPU the renderer owns alone.
+    // 2^28 (~71%) is 1-3% faster on a GPU the renderer owns alone.
     uint32_t chunk_log2 = 27;
     DevBuf wf_state;
     uint64_t kind_counters[6][8] = {};
@@ -1497,6 +1497,20 @@ void ptg_context_destroy(ptg_context* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     delete ctx;
+}
+
+int ptg_context_get_stream(ptg_context* ctx, void** out)
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_context_get_stream: null argument");
+    *out = static_cast<void*>(ctx->stream);
+    return PTG_OK;
+}
+
+int ptg_context_device(ptg_context* ctx, int* out)
+{
+    if(!ctx || !out) return fail(PTG_E_INVALID, "ptg_context_device: null argument");
+    *out = ctx->device;
+    return PTG_OK;
 }
 
 int ptg_context_set_stream(ptg_context* ctx, void* stream)

@@ -147,17 +147,34 @@ def _agree(kind, cfg, a, b, shard_rank, shard_world, group_ok, dev, what):
 
 
 def _collective_mode(shard, force_collective, what):
-    """Whether the call runs collectives: a shard of more than one rank needs
-    the default process group (and then every rank agrees on the call first,
-    _agree); a one-rank shard is rendered locally, unless it is the whole
-    group of one and `force_collective` asks for the collective anyway."""
+    """(agree, collective): whether the ranks agree on the call first
+    (_agree) and whether the data collective runs.  A shard of more than one
+    rank needs the default process group and does both.  A one-rank shard is
+    rendered locally, unless it is the whole group of one and
+    `force_collective` asks for the collective anyway; inside a larger group
+    it still joins the agreement, so a rank holding a one-rank shard while
+    the others hold shards of the group fails with them instead of leaving
+    them waiting (every rank holding a one-rank shard - replicas - agrees and
+    renders locally)."""
     import torch.distributed as dist
     grouped = dist.is_available() and dist.is_initialized()
     if shard.world == 1:
-        return bool(grouped and dist.get_world_size() == 1 and force_collective)
+        if not grouped:
+            return False, False
+        if dist.get_world_size() == 1:
+            return bool(force_collective), bool(force_collective)
+        return True, False
     if not grouped:
         raise RuntimeError("%s: world size %d but no process group" % (what, shard.world))
-    return True
+    return True, True
+
+
+def _place_ok(shard):
+    """Whether `shard` is a legitimate place for this process: its own rank of
+    the whole group, or a one-rank (replica) shard."""
+    import torch.distributed as dist
+    return shard.world == 1 and shard.rank == 0 or \
+        (dist.get_world_size() == shard.world and dist.get_rank() == shard.rank)
 
 
 def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force_collective=True):
@@ -172,7 +189,9 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
 
     A shard of more than one rank runs the collectives of the default process
     group (and a one-rank shard at world size 1 too, with `force_collective`);
-    a one-rank shard in a larger job, or with no group, is rendered locally.
+    a one-rank shard in a larger job, or with no group, is rendered locally
+    (in a larger job after the agreement: replicas agree, a rank whose
+    one-rank shard meets the others' group shards fails with them).
     Before anything is rendered the ranks agree on the call (_agree): if any
     rank's config, tile size or world size differs, or its shard is not its
     place in the group, EVERY rank raises ShardMismatch (no rank waits in a
@@ -185,12 +204,12 @@ def render_and_gather(renderer, cfg, shard: TileShard, image, stream=None, force
     import torch.distributed as dist
     dev = image.device
     per_tile = shard.tile_w * shard.tile_h
-    collective = _collective_mode(shard, force_collective, "render_and_gather")
+    agree, collective = _collective_mode(shard, force_collective, "render_and_gather")
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
     with ctx:
-        if collective:
-            _agree(1, cfg, shard.tile_w, shard.tile_h, shard.rank, shard.world,
-                   dist.get_world_size() == shard.world and dist.get_rank() == shard.rank, dev, "render_and_gather")
+        if agree:
+            _agree(1, cfg, shard.tile_w, shard.tile_h, shard.rank, shard.world, _place_ok(shard), dev,
+                   "render_and_gather")
         buf = torch.zeros((shard.max_count * per_tile, 4), dtype=torch.uint8, device=dev)
         if shard.count:
             renderer.render_tiles(cfg, shard.tile_w, shard.tile_h, shard.first, shard.stride, shard.count,
@@ -262,13 +281,12 @@ def render_and_reduce(renderer, cfg, shard: SampleShard, image, accum=None, stre
     import torch
     import torch.distributed as dist
     dev = image.device
-    collective = _collective_mode(shard, force_collective, "render_and_reduce")
+    agree, collective = _collective_mode(shard, force_collective, "render_and_reduce")
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
     with ctx:
         h, w = image.shape[0], image.shape[1]
-        if collective:
-            _agree(2, cfg, h, w, shard.rank, shard.world,
-                   dist.get_world_size() == shard.world and dist.get_rank() == shard.rank, dev, "render_and_reduce")
+        if agree:
+            _agree(2, cfg, h, w, shard.rank, shard.world, _place_ok(shard), dev, "render_and_reduce")
         part = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
         if shard.j1 > shard.j0:
             renderer.render(cfg, samples=(shard.j0, shard.j1), out_accum=part)

@@ -105,6 +105,8 @@ def lib():
         "ptg_context_create": (I, [I, C.POINTER(P)]),
         "ptg_context_destroy": (None, [P]),
         "ptg_context_set_stream": (I, [P, P]),
+        "ptg_context_get_stream": (I, [P, C.POINTER(P)]),
+        "ptg_context_device": (I, [P, C.POINTER(I)]),
         "ptg_upload_scene": (I, [P, P, P, SZ, P, SZ, P, P, P, P, SZ]),
         "ptg_upload_frame": (I, [P, P, SZ, P, SZ, P, P, SZ, SZ]),
         "ptg_upload_from_scene": (I, [P, P, I]),

@@ -75,3 +75,32 @@ def test_write_bmp_error(native_lib, tmp_path):
     import numpy as np
     img = np.zeros((2, 2, 4), np.uint8)
     assert native_lib.ptg_write_bmp(str(tmp_path / "no" / "x.bmp").encode(), 2, 2, 4, 8, img.ctypes.data) == -2
+
+
+RCCL_HEADER = os.path.join(ROOT, "include", "ptg_rccl.h")
+RCCL_LIB = os.path.join(os.path.dirname(N.LIB_PATH), "libptg_rccl.so")
+
+
+def test_rccl_library_exports_its_header_and_keeps_rccl_out_of_libptg(native_lib):
+    """include/ptg_rccl.h's entry points live in libptg_rccl.so, which links
+    librccl; libptg.so itself never needs an RCCL (torch loads its own)."""
+    text = re.sub(r"/\*.*?\*/", "", open(RCCL_HEADER).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(ptg_[a-z0-9_]+)\s*\(", text)))
+    assert declared == ["ptg_rccl_comm_destroy", "ptg_rccl_comm_init_env", "ptg_rccl_last_error", "ptg_render_gather"]
+    out = subprocess.run(["nm", "-D", "--defined-only", RCCL_LIB], stdout=subprocess.PIPE, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if line.strip())
+    assert not [f for f in declared if f not in exported]
+    needed = subprocess.run(["readelf", "-d", N.LIB_PATH], stdout=subprocess.PIPE, text=True, check=True).stdout
+    assert "rccl" not in needed
+    needed = subprocess.run(["readelf", "-d", RCCL_LIB], stdout=subprocess.PIPE, text=True, check=True).stdout
+    assert "librccl" in needed and "libptg.so" in needed
+
+
+def test_rccl_entry_points_reject_bad_arguments():
+    lib = C.CDLL(RCCL_LIB)
+    lib.ptg_rccl_last_error.restype = C.c_char_p
+    cfg = N.RenderConfig.make()
+    assert lib.ptg_render_gather(None, C.byref(cfg), 32, 16, None, None) == -1
+    assert b"null argument" in lib.ptg_rccl_last_error()
+    assert lib.ptg_rccl_comm_init_env(None, None, None, None, 1) == -1
+    assert lib.ptg_rccl_comm_destroy(None) == -1

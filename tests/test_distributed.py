@@ -259,6 +259,17 @@ def _disagree_worker(rank, world, port, case, out):
             D.render_and_gather(stub, cfg, D.TileShard(cfg, 16, 8, rank, world if rank == 0 else world + 1),
                                 torch.zeros((20, 40, 4), dtype=torch.uint8))
             rendered = bool(stub.calls)
+        elif case == "world1":    # only rank 1 holds a one-rank shard (it used to skip the agreement)
+            cfg = N.RenderConfig.make(40, 20, 8)
+            stub = StubRenderer(rank)
+            D.render_and_gather(stub, cfg, D.TileShard(cfg, 16, 8, rank, world) if rank == 0 else
+                                D.TileShard(cfg, 16, 8, 0, 1), torch.zeros((20, 40, 4), dtype=torch.uint8))
+            rendered = bool(stub.calls)
+        elif case == "replicas":  # every rank holds a one-rank shard: they agree and render locally
+            cfg = N.RenderConfig.make(40, 20, 8)
+            stub = StubRenderer(rank)
+            D.render_and_gather(stub, cfg, D.TileShard(cfg, 16, 8, 0, 1), torch.zeros((20, 40, 4), dtype=torch.uint8))
+            rendered = bool(stub.calls)
     except D.ShardMismatch as e:
         msg = str(e)
     np.save(out % rank, np.array([msg, str(rendered), str(time.monotonic() - t0)]))
@@ -266,7 +277,8 @@ def _disagree_worker(rank, world, port, case, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,field", [("tile", "disagree on tile_w"), ("spp", "disagree on spp"), ("world", "not their place")])
+@pytest.mark.parametrize("case,field", [("tile", "disagree on tile_w"), ("spp", "disagree on spp"), ("world", "not their place"),
+                                        ("world1", "disagree on world")])
 def test_disagreeing_rank_fails_every_rank(tmp_path, case, field):
     """render_and_gather / render_and_reduce: when ONE rank's call differs
     (tile size, SPP, or a shard that is not its place in the group), every
@@ -279,3 +291,13 @@ def test_disagreeing_rank_fails_every_rank(tmp_path, case, field):
         assert field in msg, (r, msg)
         assert rendered == "False"
         assert float(secs) < 30
+
+
+def test_one_rank_shards_in_a_group_render_locally(tmp_path):
+    """Replicas: every rank of a 2-rank group holds a one-rank shard; the
+    agreement passes and each rank renders its whole frame locally."""
+    out = str(tmp_path / "r%d.npy")
+    mp.spawn(_disagree_worker, args=(2, _free_port(), "replicas", out), nprocs=2, join=True)
+    for r in range(2):
+        msg, rendered, secs = np.load(out % r).tolist()
+        assert msg == "" and rendered == "True", (r, msg)

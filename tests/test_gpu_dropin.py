@@ -26,3 +26,25 @@ def test_reference_main_with_gpu_baseline_render(assets_dir, tmp_path):
     rgb = V.read_bmp(out)
     want = np.load(os.path.join(GOLDEN, "frame_160x90.npz"))["bgra"][..., [2, 1, 0]]
     assert np.array_equal(rgb, want)
+
+
+DROPIN_RCCL = os.path.join(ROOT, "oracle", "_ref", "strict_160x90_s32_b4", "dropin_rccl")
+
+
+@pytest.mark.parametrize("tile", [(32, 16), (48, 40)])
+def test_reference_main_over_rccl_gather(assets_dir, tmp_path, tile):
+    """The C++ host's multi-GPU route: the reference's own
+    host code creates an RCCL communicator from RANK / WORLD_SIZE /
+    LOCAL_RANK and calls ptg_render_gather (ptg_render_tiles -> ncclGather ->
+    ptg_scatter_tiles, include/ptg_rccl.h).  At world size 1 on this box the
+    gathered BMP equals the reference's own render byte for byte."""
+    assert os.path.exists(DROPIN_RCCL), "build the drop-in first: __graft_entry__.build() (oracle/Makefile dropin_rccl)"
+    out = tmp_path / "frame_0000.bmp"
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([DROPIN_RCCL, assets_dir, "0", str(out), str(tile[0]), str(tile[1])], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "rank 0 of 1" in r.stdout
+    rgb = V.read_bmp(out)
+    want = np.load(os.path.join(GOLDEN, "frame_160x90.npz"))["bgra"][..., [2, 1, 0]]
+    assert np.array_equal(rgb, want)

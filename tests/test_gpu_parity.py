@@ -180,3 +180,42 @@ def test_ragged_configs_bit_exact(gpu, assets_dir, w, h, spp, bounces, frame, re
     acc_o, bgra_o = Oracle(arr, s.cfg).render_rect(x0, y0, rw, rh, j0, j1)
     assert np.array_equal(_bits(acc.cpu().numpy()[..., :3]), _bits(acc_o[..., :3]))
     assert np.array_equal(bgra.cpu().numpy(), bgra_o)
+
+
+def _nan_aware_equal(a, b):
+    """Bit equality, with any NaN equal to any NaN (x86 and gfx950 quiet NaNs
+    carry different sign/payload bits)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(_bits(np.where(na, 0, a)), _bits(np.where(nb, 0, b)))
+
+
+@pytest.mark.parametrize("color,cos", [
+    ((float("nan"), 4.0, 4.0), None),        # a NaN colour component without its sign bit
+    ((1e37, 1e37, 1e37), None),              # finite, but colour x the sun disk's pdf overflows
+    ((3e38, 2.0, 1.0), None),                # near FLT_MAX: colour / mis_pdf overflows
+    ((float("inf"), 4.0, 4.0), None),
+    ((4.0, 4.0, 4.0), 1.0),                  # degenerate sun cone: the disk's pdf is infinite
+])
+def test_unvalidated_light_takes_no_shortcut(gpu, assets_dir, color, cos):
+    """the zero-throughput shortcuts (untraced moot shadow rays,
+    the skipped sky integrals, the retired last bounce) are exact only when
+    the term they skip is finite.  A light uploaded through ptg_upload_frame
+    is not validated, so a NaN, infinite or huge colour, or a cone of cos 1,
+    must take the full computation: the frame equals the oracle's (NaN where
+    it has NaN)."""
+    W, H, SPP = 48, 27, 16
+    s = scene_for(assets_dir, W, H, SPP, frame=450)
+    arr = arrays_copy(s)
+    arr["subframes"]["light"]["color"][:, :3] = np.array(color, np.float32)
+    if cos is not None:
+        arr["subframes"]["light"]["cos_solid_angle"] = np.float32(cos)
+    gpu.upload_arrays(arr)
+    bgra, acc = gpu.render(s.cfg, want_accum=True)
+    gpu.synchronize()
+    acc_o, bgra_o = Oracle(arr, s.cfg).render_rect(0, 0, W, H)
+    got = acc.cpu().numpy()[..., :3]
+    assert _nan_aware_equal(got, acc_o[..., :3])
+    fin = ~np.isnan(got).any(-1)
+    assert np.array_equal(bgra.cpu().numpy()[fin], bgra_o[fin])

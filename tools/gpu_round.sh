@@ -51,7 +51,8 @@ for step in ${STEPS:-tests smoke}; do
             PTG_LIB=$L run ab_${k}_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} || exit $?
           done
         done ;;
-    bench) run bench 1100 python bench.py || exit $? ;;
+    bench) run bench 1100 python bench.py ${BENCH_ARGS} || exit $? ;;
+    rehearse) run rehearse 1000 bash tools/rehearse.sh || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
