@@ -96,8 +96,25 @@ def frame_stats(assets, frame, y0, y1):
     }
 
 
-def metric_stats(assets, frame, w, h, spp, band=(352, 368)):
-    """T1 on a band, T2 / T3 / T3v on the whole frame, strict vs shipped, at w x h x spp."""
+def _cached(cache, name, make):
+    """make() -> tuple of arrays, saved under cache/name.npz (None: no cache)."""
+    if cache:
+        p = os.path.join(cache, name + ".npz")
+        if os.path.exists(p):
+            z = np.load(p)
+            return tuple(z["a%d" % i] for i in range(len(z.files)))
+    out = make()
+    out = out if isinstance(out, tuple) else (out,)
+    if cache:
+        os.makedirs(cache, exist_ok=True)
+        np.savez(p, **{"a%d" % i: x for i, x in enumerate(out)})
+    return out
+
+
+def metric_stats(assets, frame, w, h, spp, band=(352, 368), cache=None):
+    """T1 on a band, T2 / T3 / T3v on the whole frame, strict vs shipped, at w x h x spp.
+    `cache`: a directory keeping each build's render and band samples (hours of
+    CPU time at 1024 spp) so a rerun only recomputes the statistics."""
     from oracle import Reference
     import importlib.util
     spec = importlib.util.spec_from_file_location(
@@ -109,10 +126,13 @@ def metric_stats(assets, frame, w, h, spp, band=(352, 368)):
         if not r.available():
             raise FileNotFoundError(r.exe)
     acc, bgra = {}, {}
-    for m, r in refs.items():
-        acc[m], bgra[m] = r.render(assets, frame, timeout=6 * 3600)   # the strict build at 1024 spp: > 1 h
+    tag = "f%d_%dx%d_s%d" % (frame, w, h, spp)
+    for m, r in refs.items():   # the strict build at 1024 spp: > 1 h
+        acc[m], bgra[m] = _cached(cache, "render_%s_%s" % (m, tag), lambda r=r: r.render(assets, frame, timeout=6 * 3600))
     y0, y1 = band
-    smp = {m: r.samples(assets, frame, 0, y0, w, y1 - y0, 0, spp, timeout=6 * 3600)[..., :3] for m, r in refs.items()}
+    smp = {m: _cached(cache, "band_%s_%s_%d_%d" % (m, tag, y0, y1),
+                      lambda r=r: r.samples(assets, frame, 0, y0, w, y1 - y0, 0, spp, timeout=6 * 3600)[..., :3])[0]
+           for m, r in refs.items()}
     t1 = within(smp["strict"], smp["v3"]).all(-1)
     a_s, a_v = acc["strict"][..., :3], acc["v3"][..., :3]
     t2 = within(a_s, a_v).all(-1)
@@ -148,6 +168,7 @@ def main():
     ap.add_argument("--frames", type=int, nargs="*", default=[0, 450])
     ap.add_argument("--rows", type=int, nargs=2, default=[0, H])
     ap.add_argument("--out", default=os.path.join(HERE, "parity_stats.json"))
+    ap.add_argument("--cache", default=None, help="keep the reference builds' renders here (--metric)")
     a = ap.parse_args()
     assets = os.path.join(ROOT, "assets")
     if a.metric:
@@ -155,7 +176,7 @@ def main():
         res = json.load(open(a.out)) if os.path.exists(a.out) else {}
         rows = res.setdefault("metric_config", {"width": w, "height": h, "bounces": BOUNCES, "rows": []})["rows"]
         for f in a.frames:
-            st = metric_stats(assets, f, w, h, a.spp)
+            st = metric_stats(assets, f, w, h, a.spp, cache=a.cache)
             st["spp"] = a.spp
             rows[:] = [r for r in rows if (r["frame"], r["spp"]) != (f, a.spp)] + [st]
             rows.sort(key=lambda r: (r["spp"], r["frame"]))

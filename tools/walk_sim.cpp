@@ -322,7 +322,28 @@ struct SimWalker {
         // from the rows the ray's signs name
         const uint32_t idx = cur & kBeIndex, oc = octant(dir);
         const BlockCopy& rec = pk.E[idx];
-        const uint32_t tb = uint32_t(block_order_tables()[block_order_id(rec.a[0], rec.a[1])] >> (8 * oc)) & 0xFFu;
+        // ANYCANON=1 (model): any-hit walks take the stored (canonical) order -
+        // their result does not depend on the order (no tmax change)
+        static const bool any_canon = getenv("ANYCANON") && atoi(getenv("ANYCANON")) != 0;
+        // FLIPORDER=1 (model): the closest-hit walk takes one of two orders per
+        // block, octant 7's (canonical) or octant 0's (its reverse), by the
+        // ray's sign on the block's "best axis" (the axis whose sign alone
+        // predicts most of the eight octant orders)
+        static const bool flip_order = getenv("FLIPORDER") && atoi(getenv("FLIPORDER")) != 0;
+        const uint64_t T = block_order_tables()[block_order_id(rec.a[0], rec.a[1])];
+        uint32_t tb = (q.any && any_canon) ? 0xE4u : uint32_t(T >> (8 * oc)) & 0xFFu;
+        if(flip_order && !q.any)
+        {
+            int best = 0, agree_best = -1;
+            for(int ax = 0; ax < 3; ++ax)
+            {
+                int agree = 0;
+                for(uint32_t o = 0; o < 8; ++o)
+                    agree += ((T >> (8 * o)) & 0xFF) == ((T >> (8 * (((o >> ax) & 1u) ? 7 : 0))) & 0xFF);
+                if(agree > agree_best) { agree_best = agree; best = ax; }
+            }
+            tb = uint32_t(T >> (8 * (((oc >> best) & 1u) ? 7 : 0))) & 0xFFu;
+        }
         struct NearE { float x, y, z; uint32_t a; };
         struct { NearE n[kBlockWidth]; float f[3 * kBlockWidth]; } bc;
         for(uint32_t j = 0; j < kBlockWidth; ++j)
