@@ -72,8 +72,7 @@ constexpr uint32_t kInstAllSubframes = 0xFFFFFFFFu, kInstNoCandidate = 0xFFFFFFF
 
 // Everything a hot-path kernel reads, passed by value as a kernel argument.
 struct DevScene {
-    const BlockCopy* blocks;       // block BVH records of both levels (block_format.h), one line per block
-    const uint8_t* order_lut;      // the block order tables: kOrderTables x 8 bytes (block_format.h)
+    const BlockCopy* blocks;       // block BVH records of both levels (block_format.h), 8 copies per block
     const uint32_t* tlas_root;     // per subframe: its TLAS's root block
     const TriRec* tris;
     const TriShade* tri_shade;     // per mesh triangle, at the TriRec's index

@@ -459,24 +459,10 @@ PTG_D uint32_t sel4(uint32_t t, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t 
 // shortens tmax.  Candidates are met in the reference's order with the
 // reference's tmax (block_format.h), so the result is bit-identical to the
 // reference's stackless link walk (ray_query.hh:184-278).
-// The block order tables (block_format.h; kOrderTables x 8 bytes, table
-// byte o at id * 8 + o): read from global memory (cached) by the per-lane
-// walks, from an LDS copy by the wavefront walks.
-struct GlobalOrderLut {
-    const uint8_t* p;
-    PTG_D uint32_t at(uint32_t i) const { return p[i]; }
-};
-struct LdsOrderLut {
-    typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
-    const lds_u8_t* p;
-    PTG_D uint32_t at(uint32_t i) const { return p[i]; }
-};
-
-template<class Cold, class Stack, class Lut = GlobalOrderLut>
+template<class Cold, class Stack>
 struct BlockWalker {
     Cold cold;                 // world ray, best hit
     Stack st;
-    Lut lut;                   // the block order tables
     float tmin, tmax;
     f3 org, inv;               // active level: ray origin / 1/dir in that level's space
     f3 winv;                   // the world ray's 1/dir (the TLAS level's inv)
@@ -714,35 +700,30 @@ struct BlockWalker {
         return live && !leaf ? -1 : 0;                     // a block to step now, else nothing this phase
     }
 
-    // block cur's seven rows (block_format.h): this ray's near planes from
-    // the rows its direction's signs name (min for a positive component,
-    // else max), its far planes from the others, then the words.  32-bit
-    // byte offsets from the buffer's base (the upload keeps the block buffer
-    // below 4 GB), so the loads take the scalar-base + vector-offset form;
-    // the per-lane row offsets do the per-axis plane selection.
-    static constexpr uint32_t kBlockRows = 7;
-    PTG_D void block_offsets(uint32_t (&off)[kBlockRows]) const
+    // this octant's copy of block cur: its kBlockWidth entries in the order
+    // the ray meets them, each box as (near planes, far planes) for the
+    // octant's signs; kBlockRows 16-byte rows (seven at width 4)
+    static constexpr uint32_t kBlockRows = (28u * kBlockWidth + 15u) / 16u;
+    PTG_D const v4f* block_rows(const DevScene& sc) const
+    {   // a 32-bit byte offset from the buffer's base (the upload keeps the
+        // block buffer below 4 GB), so the loads take the scalar-base +
+        // vector-offset form instead of 64-bit address arithmetic per lane
+        const uint32_t off = (cur * kBlockCopies + oct) * uint32_t(sizeof(BlockCopy));
+        return reinterpret_cast<const v4f*>(reinterpret_cast<const uint8_t*>(sc.blocks) + off);
+    }
+    // float k of the packed far planes (rows kBlockWidth..): entry j's at 3j..3j+2
+    static PTG_D float far_plane(const v4f* q, uint32_t k)
     {
-        // (a block is 128-byte aligned: the row offsets are OR-ed in)
-        const uint32_t b = (cur & kBeIndex) * uint32_t(sizeof(BlockCopy));
-        const uint32_t no = ~oct;
-        const uint32_t sx = (no & 1u) << 4, sy = (no & 2u) << 3, sz = (no & 4u) << 2;   // 16: the near plane is the max
-        off[0] = b | sx;
-        off[1] = b | (sx ^ 16u);
-        off[2] = b | (32u | sy);
-        off[3] = b | (48u ^ sy);
-        off[4] = b | (64u | sz);
-        off[5] = b | (80u ^ sz);
-        off[6] = b | 96u;
+        const v4f r = q[kBlockWidth + k / 4u];
+        const uint32_t c = k % 4u;
+        return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w;
     }
 
     // Node phase, second half: the block step on its rows.
     template<bool COUNT>
     PTG_D int node_block(const DevScene& sc, Counters& cnt, const v4f (&q)[kBlockRows])
     {
-        // rows: near x, far x, near y, far y, near z, far z, words; entry j in
-        // lane j of each row, in the block's canonical order
-        static_assert(kBlockWidth == 4, "the row layout holds four entries");
+        // rows 0..W-1: entry j's near planes and word; then the far planes, packed
         constexpr uint32_t W = kBlockWidth;
         float4 l[W], h[W];
         uint32_t a[W];
@@ -750,12 +731,10 @@ struct BlockWalker {
 #pragma unroll
         for(uint32_t j = 0; j < W; ++j)
         {
-            l[j] = make_float4(q[0][j], q[2][j], q[4][j], 0.0f);
-            h[j] = make_float4(q[1][j], q[3][j], q[5][j], 0.0f);
-            a[j] = __float_as_uint(q[6][j]);
+            l[j] = make_float4(q[j].x, q[j].y, q[j].z, q[j].w);
+            h[j] = make_float4(far_plane(q, 3 * j), far_plane(q, 3 * j + 1), far_plane(q, 3 * j + 2), 0.0f);
+            a[j] = __float_as_uint(l[j].w);
         }
-        // the ray's order of the entries: the block's order table, byte oct
-        const uint32_t tb = lut.at(block_order_id(a[0], a[1]) * 8u + oct);
         if(COUNT) cnt.step_loads |= 1u;
         // bit j: the entry the ray meets j-th passed.  Built inside each form's
         // branch, so the two branches merge an integer, not four lane masks
@@ -794,36 +773,37 @@ struct BlockWalker {
             cnt.visits += tested;
             if(axis < 0) cnt.tlas_visits += tested;
         }
-        // In the ray's order, position p holds canonical entry e[p].  The first entry that passed
-        // in that order is walked next; the others are pushed last-first, so
-        // they pop in order.
-        uint32_t e[W], ho = 0;   // ho: bit p = the entry at position p passed
-#pragma unroll
-        for(uint32_t p = 0; p < W; ++p)
+        // The first entry that passed is walked next; the others are pushed
+        // last-first, so they pop in order.
+        const uint32_t first = uint32_t(__builtin_ctz(hits | (1u << W))) & (W - 1u);
+        uint32_t fa, fn;   // entry `first`, by value (v_cndmask): neither a branch nor an indexed copy
+        if constexpr(W == 4)
         {
-            e[p] = order_entry(tb, p);
-            ho |= ((hits >> e[p]) & 1u) << p;
+            fa = sel4(first, a[0], a[1], a[2], a[3]);
+            fn = sel4(first, __float_as_uint(nr[0]), __float_as_uint(nr[1]), __float_as_uint(nr[2]),
+                      __float_as_uint(nr[3]));
         }
-        const uint32_t first = uint32_t(__builtin_ctz(ho | (1u << W))) & (W - 1u);
-        const uint32_t ef = order_entry(tb, first);
-        // entry ef, by value (v_cndmask): neither a branch nor an indexed copy
-        const uint32_t fa = sel4(ef, a[0], a[1], a[2], a[3]);
-        const uint32_t fn = sel4(ef, __float_as_uint(nr[0]), __float_as_uint(nr[1]), __float_as_uint(nr[2]),
-                                 __float_as_uint(nr[3]));
-        cur = ho ? fa : kBePop;
+        else
+        {
+            fa = a[0];
+            fn = __float_as_uint(nr[0]);
+#pragma unroll
+            for(uint32_t j = 1; j < W; ++j)
+            {
+                fa = first == j ? a[j] : fa;
+                fn = first == j ? __float_as_uint(nr[j]) : fn;
+            }
+        }
+        cur = hits ? fa : kBePop;
         cnear = __uint_as_float(fn);
-        const uint32_t rest = ho & (ho - 1u);
+        const uint32_t rest = hits & (hits - 1u);
         if(rest)
         {   // written at the top either way, kept only if pushed
             // (the host's stack bound, which sizes the spill areas, must hold)
             PTG_CHECK(sc, st.fits(uint32_t(__builtin_popcount(rest)), sc.spill_stride), kDebugStack);
             st.reserve(W - 1);
 #pragma unroll
-            for(uint32_t p = W - 1; p >= 1; --p)
-                st.put(make_uint2(sel4(e[p], a[0], a[1], a[2], a[3]),
-                                  sel4(e[p], __float_as_uint(nr[0]), __float_as_uint(nr[1]), __float_as_uint(nr[2]),
-                                       __float_as_uint(nr[3]))),
-                       (rest >> p) & 1u);
+            for(uint32_t j = W - 1; j >= 1; --j) st.put(make_uint2(a[j], __float_as_uint(nr[j])), (rest >> j) & 1u);
         }
         park();
         return 0;
@@ -836,16 +816,11 @@ struct BlockWalker {
     PTG_D int node_step(const DevScene& sc, Counters& cnt)
     {
         if(const int r = node_pop(); r >= 0) return r;
-        PTG_CHECK(sc, (cur & kBeIndex) < sc.block_count, kDebugNode);
-        uint32_t off[kBlockRows];
-        block_offsets(off);
-        const uint8_t* base = reinterpret_cast<const uint8_t*>(sc.blocks);
+        PTG_CHECK(sc, cur < sc.block_count, kDebugNode);
+        const v4f* p = block_rows(sc);
         v4f q[kBlockRows];
-        // the words first: the order table's LDS read needs only them and
-        // then overlaps the box tests
-        q[6] = *reinterpret_cast<const v4f*>(base + off[6]);
 #pragma unroll
-        for(uint32_t k = 0; k < kBlockRows - 1; ++k) q[k] = *reinterpret_cast<const v4f*>(base + off[k]);
+        for(uint32_t k = 0; k < kBlockRows; ++k) q[k] = p[k];
         return node_block<COUNT>(sc, cnt, q);
     }
 
@@ -957,7 +932,6 @@ PTG_D bool trace(const DevScene& sc, uint32_t root, uint32_t /*unused*/, f3 o, f
 {
     if(COUNT) cnt.queries++;
     Walker w;
-    w.lut.p = sc.order_lut;
     w.init(root, o, d, tmin, tmax);
     int r;
     while((r = w.template step<ANY, COUNT>(sc, cnt)) == 0) {}

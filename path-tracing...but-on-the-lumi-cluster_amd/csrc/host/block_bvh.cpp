@@ -50,7 +50,7 @@ bool derive(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count
         if(l7.accept & 0x80000000u)
         {
             const uint32_t p = l7.accept & 0x7FFFFFFFu;
-            if(p >= payload_limit || p > kBeIndex)   // (24 bits: the order id sits above)
+            if(p >= payload_limit || p > kBeIndex)
             {
                 err = "leaf payload " + std::to_string(p) + " out of range (limit " + std::to_string(payload_limit) + ")";
                 return false;
@@ -132,141 +132,7 @@ void split_wide(Tree& t)
     }
 }
 
-// ---- entry order tables (device/block_format.h) ---------------------------
-//
-// Every order a block can need: the trees of at most kBlockWidth entries
-// whose inner nodes have 2..kBlockWidth children (a one-child node orders
-// nothing, so a block with one is ordered like the tree without it), each
-// inner node on axis x, y or z.  A table lists, per octant, the entries in
-// the order depth-first with each node's children reversed when the
-// octant's sign on its axis is not positive (bvh.cc:177-181); entry numbers
-// are canonical positions (the octant-7 order, nothing reversed).
-struct OrderTree {
-    std::vector<OrderTree> kids;   // none: an entry
-    uint32_t axis = 0;
-};
-
-void trees_with(uint32_t n, std::vector<OrderTree>& out)
-{
-    if(n == 1) out.push_back(OrderTree{});
-    for(uint32_t k = 2; k <= std::min<uint32_t>(kBlockWidth, n); ++k)
-    {   // compositions of n into k parts, each part a tree
-        std::vector<uint32_t> part(k, 1);
-        for(;;)
-        {
-            uint32_t sum = 0;
-            for(uint32_t v: part) sum += v;
-            if(sum == n)
-            {
-                std::vector<std::vector<OrderTree>> sub(k);
-                for(uint32_t i = 0; i < k; ++i) trees_with(part[i], sub[i]);
-                std::vector<size_t> pick(k, 0);
-                for(;;)
-                {
-                    OrderTree t;
-                    for(uint32_t i = 0; i < k; ++i) t.kids.push_back(sub[i][pick[i]]);
-                    out.push_back(t);
-                    uint32_t i = 0;
-                    while(i < k && ++pick[i] == sub[i].size()) pick[i++] = 0;
-                    if(i == k) break;
-                }
-            }
-            uint32_t i = 0;
-            while(i < k && ++part[i] == n) part[i++] = 1;
-            if(i == k) break;
-        }
-    }
-}
-
-std::vector<OrderTree*> inner_nodes(OrderTree& t)
-{
-    std::vector<OrderTree*> v;
-    if(t.kids.empty()) return v;
-    v.push_back(&t);
-    for(OrderTree& c: t.kids)
-        for(OrderTree* x: inner_nodes(c)) v.push_back(x);
-    return v;
-}
-
-// entry numbers in canonical (forward) order, then each octant's sequence
-void number_entries(const OrderTree& t, uint32_t& next, std::vector<uint32_t>& id, std::vector<const OrderTree*>& at)
-{
-    if(t.kids.empty())
-    {
-        at.push_back(&t);
-        id.push_back(next++);
-        return;
-    }
-    for(const OrderTree& c: t.kids) number_entries(c, next, id, at);
-}
-
-void octant_sequence(const OrderTree& t, uint32_t o, const std::vector<const OrderTree*>& at,
-                     const std::vector<uint32_t>& id, std::vector<uint32_t>& seq)
-{
-    if(t.kids.empty())
-    {
-        seq.push_back(id[size_t(std::find(at.begin(), at.end(), &t) - at.begin())]);
-        return;
-    }
-    const bool rev = ((o >> t.axis) & 1u) == 0;
-    for(size_t j = 0; j < t.kids.size(); ++j) octant_sequence(t.kids[rev ? t.kids.size() - 1 - j : j], o, at, id, seq);
-}
-
-uint64_t table_of_sequences(const std::vector<std::vector<uint32_t>>& seqs)
-{   // byte o, bits 2p..2p+1: canonical entry at position p (identity past the entries)
-    uint64_t tab = 0;
-    for(uint32_t o = 0; o < 8; ++o)
-    {
-        uint32_t byte = 0;
-        for(uint32_t p = 0; p < kBlockWidth; ++p) byte |= (p < seqs[o].size() ? seqs[o][p] : p) << (2 * p);
-        tab |= uint64_t(byte) << (8 * o);
-    }
-    return tab;
-}
-
-struct OrderTables {
-    std::vector<uint64_t> list;
-    std::unordered_map<uint64_t, uint32_t> id;
-    OrderTables()
-    {
-        for(uint32_t n = 1; n <= kBlockWidth; ++n)
-        {
-            std::vector<OrderTree> ts;
-            trees_with(n, ts);
-            for(OrderTree& t: ts)
-            {
-                std::vector<OrderTree*> in = inner_nodes(t);
-                const uint32_t combos = uint32_t(std::pow(3.0, double(in.size())) + 0.5);
-                for(uint32_t c = 0; c < combos; ++c)
-                {
-                    uint32_t r = c;
-                    for(OrderTree* x: in) { x->axis = r % 3; r /= 3; }
-                    uint32_t next = 0;
-                    std::vector<uint32_t> ids;
-                    std::vector<const OrderTree*> at;
-                    number_entries(t, next, ids, at);
-                    std::vector<std::vector<uint32_t>> seqs(8);
-                    for(uint32_t o = 0; o < 8; ++o) octant_sequence(t, o, at, ids, seqs[o]);
-                    const uint64_t tab = table_of_sequences(seqs);
-                    if(id.emplace(tab, uint32_t(list.size())).second) list.push_back(tab);
-                }
-            }
-        }
-    }
-};
-
-const OrderTables& order_tables()
-{
-    static const OrderTables t;
-    return t;
-}
-
 } // namespace
-
-const std::vector<uint64_t>& block_order_tables()
-{
-    return order_tables().list;
-}
 
 bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t block_base,
                     uint32_t payload_limit, std::vector<BlockCopy>& out, BlockBvh& info, std::string& err)
@@ -325,7 +191,7 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
             if(!t.leaf(c)) blks.push_back(make(c));
     }
     if(uint64_t(block_base) + out.size() / kBlockCopies + blks.size() > kBeIndex)
-    { err = "BVH records above 2^24 blocks"; return false; }
+    { err = "BVH records above 2^28 blocks"; return false; }
     if(out.size() % kBlockCopies) { err = "unaligned block output"; return false; }
 
     // stack bound: a block step walks one passing entry and pushes the
@@ -343,17 +209,15 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
         bound[q] = own + below;
     }
 
-    const OrderTables& tables = order_tables();
     for(const Blk& b: blks)
     {
-        // the entries in each octant's order (depth-first through the
-        // expanded nodes, each one's children forward or reversed by its
-        // axis, bvh.cc:177-181); stored once, in octant 7's (canonical)
-        // order, with the id of the table of all eight orders
-        std::vector<std::vector<uint32_t>> seqs(8);
+        // one copy per octant o: the entries in the order a ray of that
+        // octant meets them (depth-first through the expanded nodes, each
+        // one's children forward or reversed by its axis, bvh.cc:177-181),
+        // each box as (near planes, far planes) for that octant's signs
         for(uint32_t o = 0; o < 8; ++o)
         {
-            std::vector<uint32_t>& seq = seqs[o];
+            std::vector<uint32_t> seq;
             seq.reserve(W);
             auto walk = [&](auto&& self, uint32_t n) -> void {
                 const std::vector<uint32_t>& ks = t.kids[n];
@@ -368,42 +232,34 @@ bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32
             if(t.leaf(b.root)) seq.push_back(b.root);
             else walk(walk, b.root);
             if(seq.size() != b.slots.size() || seq.size() > W) { err = "block order lost an entry"; return false; }
-        }
-        const std::vector<uint32_t>& canon = seqs[7];
-        std::vector<std::vector<uint32_t>> pos(8);
-        for(uint32_t o = 0; o < 8; ++o)
-            for(uint32_t c: seqs[o])
-                pos[o].push_back(uint32_t(std::find(canon.begin(), canon.end(), c) - canon.begin()));
-        const auto it = tables.id.find(table_of_sequences(pos));
-        if(it == tables.id.end()) { err = "block entry order matches no order table"; return false; }
-        const uint32_t oid = it->second;
-        BlockCopy bc{};
-        const float inf = std::numeric_limits<float>::infinity();
-        for(uint32_t j = 0; j < W; ++j)
-        {
-            if(j >= canon.size())
-            {   // an unused slot: an empty box (min +inf, max -inf), which no
-                // ray passes in the walker's clamped test whichever planes its
-                // octant takes as near and far (BlockWalker::box_near_far); the
-                // min/max form checks kBeNone
-                for(uint32_t ax = 0; ax < 3; ++ax)
-                {
-                    bc.p[2 * ax][j] = inf;
-                    bc.p[2 * ax + 1][j] = -inf;
+            BlockCopy bc{};
+            for(uint32_t j = 0; j < W; ++j)
+            {
+                if(j >= seq.size())
+                {   // an unused slot: planes at +-inf such that, for a ray of this
+                    // octant (its reciprocal's sign per axis is the octant's), the
+                    // near plane's t is +inf and the far plane's -inf - it never
+                    // passes the walker's clamped test (BlockWalker::box_near_far);
+                    // the min/max form checks kBeNone
+                    const float inf = std::numeric_limits<float>::infinity();
+                    const bool px = o & 1u, py = o & 2u, pz = o & 4u;
+                    bc.n[j] = BlockCopy::Near{px ? inf : -inf, py ? inf : -inf, pz ? inf : -inf, kBeNone};
+                    bc.f[3 * j] = px ? -inf : inf;
+                    bc.f[3 * j + 1] = py ? -inf : inf;
+                    bc.f[3 * j + 2] = pz ? -inf : inf;
+                    continue;
                 }
-                bc.a[j] = kBeNone;
-                continue;
+                const uint32_t c = seq[j];
+                const ptg_bvh_node& n = t.box[c];
+                const bool px = o & 1u, py = o & 2u, pz = o & 4u;
+                bc.n[j] = BlockCopy::Near{px ? n.min_x : n.max_x, py ? n.min_y : n.max_y, pz ? n.min_z : n.max_z,
+                                          t.leaf(c) ? t.payload[c] : block_of[c]};
+                bc.f[3 * j] = px ? n.max_x : n.min_x;
+                bc.f[3 * j + 1] = py ? n.max_y : n.min_y;
+                bc.f[3 * j + 2] = pz ? n.max_z : n.min_z;
             }
-            const uint32_t c = canon[j];
-            const ptg_bvh_node& n = t.box[c];
-            bc.p[0][j] = n.min_x; bc.p[1][j] = n.max_x;
-            bc.p[2][j] = n.min_y; bc.p[3][j] = n.max_y;
-            bc.p[4][j] = n.min_z; bc.p[5][j] = n.max_z;
-            bc.a[j] = t.leaf(c) ? t.payload[c] : block_of[c];
+            out.push_back(bc);
         }
-        bc.a[0] |= (oid & 15u) << kBeOrderShift;
-        bc.a[1] |= (oid >> 4) << kBeOrderShift;
-        out.push_back(bc);
     }
     info.root = block_base + uint32_t((out.size() / kBlockCopies) - blks.size());
     info.blocks = uint32_t(blks.size());
@@ -464,8 +320,8 @@ static void dedup_tlas(FramePack& fp)
     {   // BFS within each TLAS: a block's children come after it
         memcpy(tmp, &fp.tlas[k * E], sizeof(tmp));
         for(BlockCopy& c: tmp)
-            for(uint32_t& e: c.a)
-                if(!(e & (kBeLeaf | kBeNone))) e = (e & ~kBeIndex) | canon[(e & kBeIndex) - fp.tlas_base];
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a = canon[e.a - fp.tlas_base];
         uint64_t h = 1469598103934665603ull;   // FNV-style mix over the block's 64-bit words
         static_assert(sizeof(tmp) % 8 == 0, "whole words");
         for(size_t i = 0; i < sizeof(tmp); i += 8)
@@ -499,8 +355,8 @@ static void dedup_tlas(FramePack& fp)
         for(size_t j = 0; j < E; ++j)
         {
             BlockCopy c = uniq[size_t(id) * E + j];
-            for(uint32_t& e: c.a)
-                if(!(e & (kBeLeaf | kBeNone))) e = (e & ~kBeIndex) | (fp.tlas_base + pos[e & kBeIndex]);
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a = fp.tlas_base + pos[e.a];
             out[size_t(pos[id]) * E + j] = c;
         }
     for(uint32_t& r: fp.tlas_root) r = fp.tlas_base + pos[canon[r - fp.tlas_base]];
@@ -597,11 +453,11 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
     for(size_t i = 0; i < subframe_count; ++i)
     {
         const uint32_t base = fp.tlas_base + uint32_t(fp.tlas.size() / kBlockCopies);
-        if(uint64_t(base) + part[i].size() / kBlockCopies > kBeIndex) { err = "TLAS records above 2^24 blocks"; return PTG_E_RANGE; }
+        if(uint64_t(base) + part[i].size() / kBlockCopies > kBeIndex) { err = "TLAS records above 2^28 blocks"; return PTG_E_RANGE; }
         for(BlockCopy c: part[i])
         {
-            for(uint32_t& e: c.a)
-                if(!(e & (kBeLeaf | kBeNone))) e += base;   // (the index stays below 2^24: checked above)
+            for(BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone))) e.a += base;
             fp.tlas.push_back(c);
         }
         fp.tlas_root[i] = pinfo[i].root + base;
@@ -613,8 +469,8 @@ int BlockCache::pack_frame(const ptg_bvh_node* static_nodes, const ptg_bvh_link*
     const uint32_t total = fp.total_blocks();
     for(const std::vector<BlockCopy>* v: {&fp.new_blas, &fp.tlas})
         for(const BlockCopy& c: *v)
-            for(uint32_t e: c.a)
-                if(!(e & (kBeLeaf | kBeNone)) && (e & kBeIndex) >= total) { err = "block link outside the block buffer"; return PTG_E_RANGE; }
+            for(const BlockCopy::Near& e: c.n)
+                if(!(e.a & (kBeLeaf | kBeNone)) && e.a >= total) { err = "block link outside the block buffer"; return PTG_E_RANGE; }
     for(uint32_t r: fp.tlas_root)
         if(r >= total) { err = "TLAS root outside the block buffer"; return PTG_E_RANGE; }
     for(uint32_t r: fp.inst_root)

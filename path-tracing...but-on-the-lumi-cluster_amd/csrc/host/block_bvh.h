@@ -16,22 +16,15 @@ struct BlockBvh {
     uint32_t max_payload = 0;   // largest leaf payload
 };
 
-// The kOrderTables entry order tables (device/block_format.h), indexed by
-// order id: byte o, bits 2p..2p+1 = the canonical entry a ray of octant o
-// meets p-th.  The device walks read them from LDS (ptg_context uploads them).
-const std::vector<uint64_t>& block_order_tables();
-
 // Packs one BVH given in the reference layout - nodes[0..count) and the eight
 // link orders links[o * count + i] (bvh.cc:195-229) - appending its blocks
-// (one 128-byte record each, entries in canonical order + an order id) to
-// `out`.  Child block indices are block_base + position in `out`.  Checked,
-// with an error in `err`:
+// (kBlockCopies copies each, one per octant) to `out`.  Child block
+// indices are block_base + position in `out` / kBlockCopies.  Checked, with an error in `err`:
 //   - the links are the reference builder's: a tree rooted at node 0 whose
 //     every order lists each node's children forward, or reversed when the
 //     octant's sign on the node's axis is not positive (bvh.cc:173-191);
 //   - every box contains its children's boxes (the walk skips inner boxes);
-//   - leaf payloads are below payload_limit (and 2^24);
-//   - every block's eight orders are one of the order tables.
+//   - leaf payloads are below payload_limit (and 2^28).
 bool pack_block_bvh(const ptg_bvh_node* nodes, const ptg_bvh_link* links, uint32_t count, uint32_t block_base,
                     uint32_t payload_limit, std::vector<BlockCopy>& out, BlockBvh& info, std::string& err);
 

@@ -321,18 +321,8 @@ __global__ __launch_bounds__(kBlock) PTG_WALK_ATTR void k_wf_walk(DevScene sc, P
     // LDS: every lane's world ray, then the stack windows, one 64-lane x kCap
     // entry table per wave (ptg_context_create sizes the block's LDS)
     extern __shared__ WalkCold cold[];
-    typedef typename WalkStackOf<ANY>::type WalkStack;
-    BlockWalker<LdsCold, WalkStack, LdsOrderLut> w;
+    BlockWalker<LdsCold, typename WalkStackOf<ANY>::type> w;
     w.cold.c = (lds_cold_t*)(&cold[threadIdx.x]);   // C cast: generic -> LDS address space
-    {   // the block order tables (kOrderTables x 8 bytes) after the stack
-        // windows: every block step reads its order byte from them
-        uint32_t* lut = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(cold) +
-                                                    blockDim.x * (sizeof(WalkCold) + WalkStack::kLaneBytes));
-        for(uint32_t i = threadIdx.x; i < kOrderTables * 2u; i += blockDim.x)
-            lut[i] = reinterpret_cast<const uint32_t*>(sc.order_lut)[i];
-        __syncthreads();
-        w.lut.p = (const LdsOrderLut::lds_u8_t*)(reinterpret_cast<const uint8_t*>(lut));   // C cast: generic -> LDS
-    }
     w.st.bind(cold + blockDim.x, threadIdx.x >> 6, lane, sc.spill + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * sc.spill_stride);
     bool active = false;
     uint32_t q = 0;
@@ -887,7 +877,6 @@ struct ptg_context {
     bool scene_ready = false;
     // frame: blocks = [BLAS blocks][this frame's TLAS blocks]
     DevBuf blocks, tlas_root, subframes, inst_trav, inst_shade, inst_box, jobs, polygon, spill;
-    DevBuf order_lut;                      // the block order tables (block_format.h), uploaded once
     HostStage stage[2];                                  // ptg_upload_frame's pinned staging, used alternately
     uint32_t stage_next = 0;
     size_t block_count = 0, subframe_count = 0, instance_count = 0;
@@ -995,7 +984,6 @@ struct ptg_context {
     {
         DevScene s;
         s.blocks = blocks.as<BlockCopy>();
-        s.order_lut = order_lut.as<uint8_t>();
         s.tlas_root = tlas_root.as<uint32_t>();
         s.tris = tris.as<TriRec>();
         s.tri_shade = tri_shade.as<TriShade>();
@@ -1447,8 +1435,8 @@ int ptg_context_create(int device, ptg_context** out)
     // window (8 x kCap B) in LDS, so the walk blocks' LDS sets how many are
     // resident per CU: kWalkResident (the LDS is padded to that share).
     const uint32_t lds_cu = prop.maxSharedMemoryPerMultiProcessor ? uint32_t(prop.maxSharedMemoryPerMultiProcessor) : 65536u;
-    const uint32_t lds_need[2] = {kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<false>::type::kLaneBytes) + kOrderTables * 8u,
-                                  kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<true>::type::kLaneBytes) + kOrderTables * 8u};
+    const uint32_t lds_need[2] = {kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<false>::type::kLaneBytes),
+                                  kBlock * uint32_t(sizeof(WalkCold) + WalkStackOf<true>::type::kLaneBytes)};
     for(int k = 0; k < 2; ++k)
     {
         const uint32_t resident = env_knob(k ? "PTG_WALK_RESIDENT_ANY" : "PTG_WALK_RESIDENT", kWalkResident[k]);
@@ -1479,12 +1467,6 @@ int ptg_context_create(int device, ptg_context** out)
     PTG_HIP(ctx->debug.reserve(kDebugSlots * sizeof(uint32_t)));
     PTG_HIP(hipMemset(ctx->debug.p, 0, kDebugSlots * sizeof(uint32_t)));
 #endif
-    {   // the block order tables, once (the packer's ids index them)
-        const std::vector<uint64_t>& tabs = block_order_tables();
-        if(tabs.size() != kOrderTables) return fail(PTG_E_INVALID, "block order tables: unexpected count");
-        PTG_HIP(ctx->order_lut.reserve(tabs.size() * sizeof(uint64_t)));
-        PTG_HIP(hipMemcpy(ctx->order_lut.p, tabs.data(), tabs.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    }
     PTG_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
     PTG_HIP(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
     PTG_HIP(hipEventCreateWithFlags(&ctx->ev_side, hipEventDisableTiming));
@@ -1733,7 +1715,7 @@ int upload_frame(ptg_context* ctx, const ptg_subframe* subframes, size_t subfram
     const std::vector<BlockCopy>& old_blas = ctx->cache.blas;
     const size_t blas_total = old_blas.size() + fp.new_blas.size();
     const size_t need = (blas_total + fp.tlas.size()) * sizeof(BlockCopy);
-    if(need > 0xFFFFFFFFull)   // the walks address blocks by 32-bit byte offsets (BlockWalker::block_offsets)
+    if(need > 0xFFFFFFFFull)   // the walks address blocks by 32-bit byte offsets (BlockWalker::block_rows)
         return fail(PTG_E_RANGE, "block records above 4 GB (" + std::to_string(need) + " B)");
     if(need > ctx->blocks.bytes)
     {

@@ -59,6 +59,18 @@ def test_lockstep_schedule_model_exact(walk_sim, assets_dir):
     assert len(lanes) == 2 and all(20 < x < 64 for x in lanes), r.stdout
 
 
+def test_eight_wide_blocks_exact(native_lib, assets_dir):
+    """8-wide blocks (measured slower on the GPU) meet
+    every leaf in the reference's order too: the packer and the walk are
+    generic in the block width."""
+    subprocess.run(["make", "-s", "walk_sim8"], cwd=os.path.join(ROOT, "tools"), check=True)
+    r = subprocess.run([os.path.join(ROOT, "tools", "_bin", "walk_sim8"), assets_dir, "450", "1500", "16"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"(\d+) queries, (\d+) mismatches", r.stdout)
+    assert m and int(m.group(2)) == 0, r.stdout
+
+
 def test_zero_and_nan_direction_components(walk_sim, assets_dir):
     """A ray with a zero direction component (1/dir infinite) takes the
     walk's min/max form of the slab test (BlockWalker::node_block).  Bounces

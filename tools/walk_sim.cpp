@@ -202,6 +202,7 @@ std::vector<uint64_t>* g_lines = nullptr;  // CACHESIM: the 128-byte lines a ste
 
 struct Packed {
     std::vector<BlockCopy> E;          // the device block buffer: [BLAS blocks][TLAS blocks]
+    std::vector<uint8_t> order_axes;   // per block: the axes whose sign changes its entry order (COPIES=v model)
     std::vector<uint32_t> inst_root;   // per instance: BLAS root block
     std::vector<uint32_t> tlas_root;   // per subframe
 };
@@ -315,51 +316,26 @@ struct SimWalker {
         st.steps++;
         st.block_steps++;
         st.bytes += 128;
-        if(g_visits) g_visits->insert((uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | (cur & kBeIndex));
-        g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | (cur & kBeIndex);
-        // the block's one record (block_format.h): entries in canonical order,
-        // the ray's order from the block's order table; near / far planes
-        // from the rows the ray's signs name
-        const uint32_t idx = cur & kBeIndex, oc = octant(dir);
-        const BlockCopy& rec = pk.E[idx];
-        // ANYCANON=1 (model): any-hit walks take the stored (canonical) order -
-        // their result does not depend on the order (no tmax change)
-        static const bool any_canon = getenv("ANYCANON") && atoi(getenv("ANYCANON")) != 0;
-        // FLIPORDER=1 (model): the closest-hit walk takes one of two orders per
-        // block, octant 7's (canonical) or octant 0's (its reverse), by the
-        // ray's sign on the block's "best axis" (the axis whose sign alone
-        // predicts most of the eight octant orders)
-        static const bool flip_order = getenv("FLIPORDER") && atoi(getenv("FLIPORDER")) != 0;
-        const uint64_t T = block_order_tables()[block_order_id(rec.a[0], rec.a[1])];
-        uint32_t tb = (q.any && any_canon) ? 0xE4u : uint32_t(T >> (8 * oc)) & 0xFFu;
-        if(flip_order && !q.any)
-        {
-            int best = 0, agree_best = -1;
-            for(int ax = 0; ax < 3; ++ax)
-            {
-                int agree = 0;
-                for(uint32_t o = 0; o < 8; ++o)
-                    agree += ((T >> (8 * o)) & 0xFF) == ((T >> (8 * (((o >> ax) & 1u) ? 7 : 0))) & 0xFF);
-                if(agree > agree_best) { agree_best = agree; best = ax; }
-            }
-            tb = uint32_t(T >> (8 * (((oc >> best) & 1u) ? 7 : 0))) & 0xFFu;
+        if(g_visits) g_visits->insert((uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur);
+        g_last_block = (uint64_t(axis < 0 ? 0xFFFFFFFFu : b.id) << 32) | cur;
+        // the ray octant's copy: entries in the ray's order, boxes as (near, far) planes
+        const BlockCopy& bc = pk.E[size_t(cur) * kBlockCopies + octant(dir)];
+        if(g_lines)
+        {   // the copy's 128 B lines.  COPIES (model only):
+            // 8 = one copy per ray octant (the shipped layout); 2 = one per sign
+            // of the ray's x direction; 1 = a single copy per block (its order
+            // for the ray's octant from an order word in the same line)
+            static const uint32_t copies = getenv("COPIES") ? uint32_t(atoi(getenv("COPIES"))) : kBlockCopies;
+            // COPIES=0: one copy per distinct entry order of the block (its
+            // order depends only on the signs of the axes in order_axes):
+            // copy (octant & mask), 2^popcount(mask) lines per block
+            const uint32_t sub = copies == 8 ? octant(dir) : copies == 2 ? (dir.x > 0 ? 1u : 0u)
+                                 : copies == 4 ? (octant(dir) & 3u)
+                                 : copies == 0 ? (octant(dir) & pk.order_axes[cur]) : 0u;
+            const size_t span = copies == 0 ? 8u : copies;
+            for(size_t k = 0; k < sizeof(BlockCopy) / 128; ++k)
+                g_lines->push_back((size_t(cur) * span + sub) * (sizeof(BlockCopy) / 128) + k);
         }
-        struct NearE { float x, y, z; uint32_t a; };
-        struct { NearE n[kBlockWidth]; float f[3 * kBlockWidth]; } bc;
-        for(uint32_t j = 0; j < kBlockWidth; ++j)
-        {
-            const uint32_t e = order_entry(tb, j);
-            float nv[3], fv[3];
-            for(uint32_t ax = 0; ax < 3; ++ax)
-            {
-                const bool pos = (oc >> ax) & 1u;
-                nv[ax] = rec.p[2 * ax + (pos ? 0 : 1)][e];
-                fv[ax] = rec.p[2 * ax + (pos ? 1 : 0)][e];
-                bc.f[3 * j + ax] = fv[ax];
-            }
-            bc.n[j] = NearE{nv[0], nv[1], nv[2], rec.a[e]};
-        }
-        if(g_lines) g_lines->push_back(idx);   // the record's 128 B line
         const bool fin = std::isfinite(inv.x) && std::isfinite(inv.y) && std::isfinite(inv.z);
         uint32_t cand = kBePop;
         float cn = 0;
@@ -378,7 +354,7 @@ struct SimWalker {
             int ne = 0;
             for(uint32_t j = 0; j < kBlockWidth; ++j)
             {
-                const auto& x = bc.n[j];
+                const BlockCopy::Near& x = bc.n[j];
                 const float* xf = &bc.f[3 * j];
                 if(x.a & kBeNone) continue;
                 float n;
@@ -403,7 +379,7 @@ struct SimWalker {
         }
         for(int j = int(kBlockWidth) - 1; j >= 0; --j)
         {
-            const auto& x = bc.n[j];
+            const BlockCopy::Near& x = bc.n[j];
             const float* xf = &bc.f[3 * j];
             if(x.a & kBeNone) continue;
             float n;
@@ -602,7 +578,26 @@ int main(int argc, char** argv)
     pk.E = cache.blas;
     pk.E.insert(pk.E.end(), fp.new_blas.begin(), fp.new_blas.end());
     pk.E.insert(pk.E.end(), fp.tlas.begin(), fp.tlas.end());
-    printf("blocks %zu (%.1f MB)\n", pk.E.size(), pk.E.size() * sizeof(BlockCopy) / 1e6);
+    {   // per block: the axes a whose sign flip changes some octant's entry order
+        const size_t nb = pk.E.size() / kBlockCopies;
+        pk.order_axes.assign(nb, 0);
+        double lines = 0;
+        size_t hist[8] = {};
+        for(size_t k = 0; k < nb; ++k)
+        {
+            uint8_t m = 0;
+            for(uint32_t o = 0; o < 8; ++o)
+                for(uint32_t a = 0; a < 3; ++a)
+                    for(uint32_t j = 0; j < kBlockWidth; ++j)
+                        if(pk.E[k * 8 + o].n[j].a != pk.E[k * 8 + (o ^ (1u << a))].n[j].a) m |= uint8_t(1u << a);
+            pk.order_axes[k] = m;
+            lines += double(1u << __builtin_popcount(m));
+            hist[m]++;
+        }
+        printf("blocks %zu: distinct orders per block %.2f on average; axis masks", nb, lines / double(nb));
+        for(int m = 0; m < 8; ++m) printf(" %d:%zu", m, hist[m]);
+        printf("\n");
+    }
     pk.inst_root = fp.inst_root;
     pk.tlas_root = fp.tlas_root;
     {   // the any-hit candidates' requirement (the upload checks it per BLAS and mesh)
