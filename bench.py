@@ -33,7 +33,12 @@ Beside `value` the line carries (rank 0):
   cpu_baseline      the reference's own baseline_render built from its sources,
                     timed on this host's cores (bounded samples).
 
-Multi-GPU: one process per GPU (torch.distributed.run).  --shard frames
+Multi-GPU: one process per GPU (torch.distributed.run).  `--gpus N` with N >
+1 and no WORLD_SIZE in the environment starts the N ranks itself (a child
+torch.distributed.run, before anything touches a GPU) and forwards its
+output and exit code; a WORLD_SIZE that is not --gpus exits with status 2.
+At N > 1 the line also carries `strong`: the metric frame in interleaved
+tiles over the same ranks, gathered on rank 0 by one RCCL gather.  --shard frames
 (default): rank r renders frame (frame + r) - weak scaling, no collective on
 the data path (BASELINE config 4 style).  --shard tiles: one frame split into
 interleaved 32x16 tiles, rank 0 gathers the BGRA tiles over RCCL and
@@ -568,9 +573,14 @@ def main():
         want = frame_golden(cfg, f)
         if want is None:
             return None
-        got = image_hashes(accum.cpu().numpy(), image.cpu().numpy())
+        acc_host = accum.cpu().numpy()
+        got = image_hashes(acc_host, image.cpu().numpy())
+        # pixels whose accumulated radiance is NaN: a path that met a zero BSDF
+        # pdf turns its sample, and so its pixel's sum, into NaN - in the
+        # reference too (path_tracer.hh:735-737, main.cc:42)
+        nan_px = int(np.isnan(acc_host[..., :3]).any(-1).sum())
         return {"frame": f, "exact": got == want, "radiance": got["sha_radiance"] == want["sha_radiance"],
-                "bgra": got["sha_bgra"] == want["sha_bgra"],
+                "bgra": got["sha_bgra"] == want["sha_bgra"], "nan_pixels": nan_px,
                 "golden": "tests/golden/full_render_s1024.json (the reference's strict build, whole image)"}
 
     def walk_levels(kind, workload, busy_ms, launches, iso_ms):
@@ -926,6 +936,7 @@ def main():
             "heavy_ms": heavy["ms_per_step"] if heavy else None,
             "heavy_value": heavy["value"] if heavy else None,
             "heavy_frame_exact": (heavy.get("frame_check") or {}).get("exact") if heavy else None,
+            "nan_pixels": [(main_check or {}).get("nan_pixels"), ((heavy or {}).get("frame_check") or {}).get("nan_pixels")],
             "anim_frames_per_min": anim["frames_per_min"] if anim else None,
             "anim_spots": anim["spots_exact"] if anim else None,
             "strong_value": strong["value"] if strong else None,

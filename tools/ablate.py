@@ -15,6 +15,7 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--pipeline", default="wavefront")
 ap.add_argument("--counters", action="store_true")
 ap.add_argument("--concurrency", type=int, default=2)
+ap.add_argument("--owned", action="store_true", help="the bench's owned-GPU chunking: 2^28 paths, 40%% HBM share")
 a = ap.parse_args()
 import torch  # noqa
 import ptlumi_loader  # noqa
@@ -23,6 +24,8 @@ from ptlumi.renderer import GpuRenderer
 cfg = N.RenderConfig.make(a.width, a.height, a.spp, a.bounces)
 s = N.Scene(os.path.join(ROOT, "assets"), cfg); s.setup_frame(a.frame)
 r = GpuRenderer(0); r.upload(s); r.set_pipeline(a.pipeline); r.set_concurrency(a.concurrency)
+if a.owned:
+    r.set_hbm_share(40); r.set_chunk_paths(28)
 img, _ = r.render(cfg); r.synchronize()
 r.enable_timing(True)
 best, kt = 1e30, None

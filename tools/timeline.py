@@ -25,7 +25,8 @@ def kind(name):
 ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind(r["Kernel_Name"])) for r in rows]
 ev.sort()
 cams = [e for e in ev if e[2] == "camera"]
-t0 = cams[-8][0]   # the last frame: its 8 chunks' camera launches
+import os
+t0 = cams[-int(os.environ.get("TL_CHUNKS", "8"))][0]   # the last frame: its chunks' camera launches (8 at 2^27 paths, 4 at 2^28)
 frame = [e for e in ev if e[0] >= t0 and e[2] not in ("fillBufferAligned", "copyBuffer")]
 t1 = max(e[1] for e in frame)
 wall = (t1 - t0) / 1e6
