@@ -1181,13 +1181,61 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     auto cnt_for = [&](int kind) { return cnt_dev ? cnt_dev + 8 * kind : nullptr; };
     auto ws_for = [&](bool any) { return cnt_dev ? cnt_dev + 8 * K_KINDS + (any ? WS_COUNT : 0) : nullptr; };
     unsigned long long* const redo_tally = cnt_dev ? cnt_dev + 8 * K_KINDS + 2 * WS_COUNT : nullptr;
-    uint32_t chunk_index = 0;
-    for(uint32_t j = j0; j < j1; j += chunk, ++chunk_index)
+    // The chunk plan: (first sample, samples, slot), in sample order (the
+    // order the chunks are folded).  With one slot, or chunks too small to
+    // halve into whole motion-blur groups: equal chunks dealt round-robin.
+    // With two slots: staggered - slot 1 starts and ends with half a chunk,
+    // so the two pipelines never change chunks at the same moment (a change
+    // runs the previous chunk's fold and the next chunk's camera kernel, with
+    // no walk of that slot in flight: when both slots changed together the
+    // GPU ran no walk for ~8 ms, profiles/r06c_timeline/).  The sample ranges
+    // follow the chunks' expected completion order (equal cost per sample),
+    // so each slot's next chunk finds its previous chunk already folded.
+    struct Piece { uint32_t j, n, slot; };
+    std::vector<Piece> plan;
+    if(nslots == 2 && chunk >= 16 && chunk % 16 == 0 && span > chunk)
     {
-        const uint32_t nj = std::min(chunk, j1 - j);
-        ptg_context::Slot& sl = slots[chunk_index % nslots];
-        SlotState& sst = st[chunk_index % nslots];
-        const DevScene sc_ext = walk_scene(chunk_index % nslots, 0), sc_sh = walk_scene(chunk_index % nslots, 1);
+        struct Nominal { uint64_t done; uint32_t slot, n; };
+        std::vector<Nominal> nom;
+        // each slot takes half of the span; slot 1's first piece is half a chunk
+        const uint32_t span1 = (span / 2) & ~7u, span0 = span - span1;
+        uint64_t t = 0;
+        for(uint32_t left = span0; left > 0;)
+        {
+            const uint32_t n = std::min(chunk, left);
+            t += n;
+            nom.push_back({t, 0u, n});
+            left -= n;
+        }
+        t = 0;
+        for(uint32_t left = span1, first = 1; left > 0; first = 0)
+        {
+            const uint32_t n = std::min(first ? chunk / 2 : chunk, left);
+            t += n;
+            nom.push_back({t, 1u, n});
+            left -= n;
+        }
+        std::stable_sort(nom.begin(), nom.end(), [](const Nominal& a, const Nominal& b) {
+            return a.done < b.done || (a.done == b.done && a.slot < b.slot); });
+        uint32_t j = j0;
+        for(const Nominal& x: nom)
+        {
+            if(j >= j1) break;
+            const uint32_t n = std::min(x.n, j1 - j);
+            plan.push_back({j, n, x.slot});
+            j += n;
+        }
+        if(j != j1) plan.clear();   // (never: the pieces cover span0 + span1 = span)
+    }
+    if(plan.empty())
+        for(uint32_t j = j0, k = 0; j < j1; j += chunk, ++k) plan.push_back({j, std::min(chunk, j1 - j), k % nslots});
+    uint32_t slot_chunks[ptg_context::kMaxSlots] = {};
+    for(const Piece& pc: plan)
+    {
+        const uint32_t j = pc.j, nj = pc.n, si = pc.slot;
+        ptg_context::Slot& sl = slots[si];
+        SlotState& sst = st[si];
+        const DevScene sc_ext = walk_scene(si, 0), sc_sh = walk_scene(si, 1);
         PathSoA* S = sst.S;
         TraceOut* trs = sst.trs;
         uint32_t** lists = sst.lists;
@@ -1195,7 +1243,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         uint32_t* sky_list = sst.sky_list;
         uint32_t* counts = sst.counts;
         const hipStream_t ms = sl.main;
-        if(nslots > 1 && chunk_index >= nslots)
+        if(nslots > 1 && slot_chunks[si]++ > 0)
             PTG_HIP(hipStreamWaitEvent(ms, sl.ev_acc, 0));   // its samples buffer was folded in
         const size_t lanes = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8) * 64;
         float4* out = sl.samples->as<float4>();

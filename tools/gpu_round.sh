@@ -48,7 +48,7 @@ for step in ${STEPS:-tests smoke}; do
           k=$((k+1))   # run index: a library named twice (interleaved repeats) keeps both outputs
           for f in ${FRAMES:-0 450}; do
             if [ "$lib" = default ]; then L=""; else L=$P/ablate_$lib/libptg.so; fi
-            PTG_LIB=$L run ab_${k}_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} || exit $?
+            PTG_LIB=$L run ab_${k}_${lib}_f$f 300 python tools/ablate.py --spp ${SPP:-1024} --frame $f --reps ${REPS:-2} ${ABARGS} || exit $?
           done
         done ;;
     bench) run bench 1100 python bench.py ${BENCH_ARGS} || exit $? ;;
