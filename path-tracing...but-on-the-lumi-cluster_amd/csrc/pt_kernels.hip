@@ -1193,7 +1193,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     // so each slot's next chunk finds its previous chunk already folded.
     struct Piece { uint32_t j, n, slot; };
     std::vector<Piece> plan;
-    if(nslots == 2 && chunk >= 16 && chunk % 16 == 0 && span > chunk)
+#ifndef PTG_STAGGER
+#define PTG_STAGGER 1   // 0: equal chunks round-robin (timing variants)
+#endif
+    if(PTG_STAGGER && nslots == 2 && chunk >= 16 && chunk % 16 == 0 && span > chunk)
     {
         struct Nominal { uint64_t done; uint32_t slot, n; };
         std::vector<Nominal> nom;
@@ -1229,10 +1232,54 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     }
     if(plan.empty())
         for(uint32_t j = j0, k = 0; j < j1; j += chunk, ++k) plan.push_back({j, std::min(chunk, j1 - j), k % nslots});
-    uint32_t slot_chunks[ptg_context::kMaxSlots] = {};
+    // Folds (k_accumulate, chunks in sample order on the accumulation stream)
+    // are issued lazily: a chunk's fold goes out just before the next chunk of
+    // its slot (which waits for it: it reuses the samples buffer), or at the
+    // end.  Issued right after its chunk, a fold's wait would sit in the
+    // accumulation stream ahead of the other slot's next launches, and HIP
+    // may map those two streams onto one hardware queue (GPU_MAX_HW_QUEUES 4):
+    // the other slot's first chunk then waited for this slot's whole chunk
+    // (profiles/r06c_timeline/).
+    std::vector<uint32_t> pending;
+    uint32_t last_of_slot[ptg_context::kMaxSlots];
+    for(uint32_t& v: last_of_slot) v = 0xFFFFFFFFu;
+    auto fold = [&](uint32_t k) -> int {
+        const Piece& pf = plan[k];
+        ptg_context::Slot& sl = slots[pf.slot];
+        const int first = pf.j == j0, last = pf.j + pf.n >= j1;
+        hipStream_t as = sl.main;
+        if(nslots > 1)
+        {
+            as = ctx->acc_stream;
+            PTG_HIP(hipStreamWaitEvent(as, sl.ev_done, 0));
+        }
+        if(int r = timed_begin(ctx, K_ACCUM, as)) return r;
+        hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, as, pm, pf.n,
+                           sl.samples->as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
+                           reinterpret_cast<float4*>(out_accum), reinterpret_cast<uchar4*>(out_bgra));
+        PTG_HIP(hipGetLastError());
+        if(int r = timed_end(ctx, as)) return r;
+        if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_acc, as));
+        return PTG_OK;
+    };
+    // issue the pending folds of chunks 0 .. upto - 1 of the plan, in order
+    auto flush_folds = [&](uint32_t upto) -> int {
+        size_t n = 0;
+        while(n < pending.size() && pending[n] < upto)
+        {
+            if(int r = fold(pending[n])) return r;
+            ++n;
+        }
+        pending.erase(pending.begin(), pending.begin() + n);
+        return PTG_OK;
+    };
     for(const Piece& pc: plan)
     {
         const uint32_t j = pc.j, nj = pc.n, si = pc.slot;
+        if(last_of_slot[si] != 0xFFFFFFFFu)   // this slot's previous chunk is folded first (samples buffer)
+            if(int r = flush_folds(last_of_slot[si] + 1)) return r;
+        const bool slot_busy = last_of_slot[si] != 0xFFFFFFFFu;
+        last_of_slot[si] = uint32_t(&pc - plan.data());
         ptg_context::Slot& sl = slots[si];
         SlotState& sst = st[si];
         const DevScene sc_ext = walk_scene(si, 0), sc_sh = walk_scene(si, 1);
@@ -1243,7 +1290,7 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         uint32_t* sky_list = sst.sky_list;
         uint32_t* counts = sst.counts;
         const hipStream_t ms = sl.main;
-        if(nslots > 1 && slot_chunks[si]++ > 0)
+        if(nslots > 1 && slot_busy)
             PTG_HIP(hipStreamWaitEvent(ms, sl.ev_acc, 0));   // its samples buffer was folded in
         const size_t lanes = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8) * 64;
         float4* out = sl.samples->as<float4>();
@@ -1362,23 +1409,14 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
             }
         }
-        // fold the chunk into the running per-pixel sums, chunks in sample order
-        const int first = j == j0, last = j + nj >= j1;
-        hipStream_t as = ms;
-        if(nslots > 1)
-        {
-            as = ctx->acc_stream;
-            PTG_HIP(hipEventRecord(sl.ev_done, ms));
-            PTG_HIP(hipStreamWaitEvent(as, sl.ev_done, 0));
-        }
-        if(int r = timed_begin(ctx, K_ACCUM, as)) return r;
-        hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, as, pm, nj,
-                           sl.samples->as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
-                           reinterpret_cast<float4*>(out_accum), reinterpret_cast<uchar4*>(out_bgra));
-        PTG_HIP(hipGetLastError());
-        if(int r = timed_end(ctx, as)) return r;
-        if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_acc, as));
+        // the chunk's fold into the running per-pixel sums is issued later
+        // (fold below), in sample order
+        if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_done, ms));
+        pending.push_back(uint32_t(&pc - plan.data()));
+        if(nslots == 1)
+            if(int r = flush_folds(uint32_t(plan.size()))) return r;
     }
+    if(int r = flush_folds(uint32_t(plan.size()))) return r;
     if(nslots > 1)
     {   // the caller's stream sees the whole render
         PTG_HIP(hipEventRecord(ctx->ev_acc_end, ctx->acc_stream));
