@@ -916,11 +916,12 @@ struct ptg_context {
     // Wavefront chunk pipelines ("slots").  With two slots, consecutive
     // chunks run concurrently on their own stream pairs and buffers, so one
     // chunk's round-0 walk and shade overlap the other's sky and shadow
-    // kernels; k_accumulate still folds the chunks in sample order, on
-    // acc_stream.  Slot 0 is the context's own stream pair and buffers.
+    // kernels; k_accumulate still folds the chunks in sample order, each on
+    // its chunk's slot stream, chained by events across the slots (render_map).
+    // Slot 0 is the context's own stream pair and buffers.
     struct Slot {
         hipStream_t main = nullptr, side = nullptr;
-        hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_done = nullptr, ev_acc = nullptr;
+        hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_acc = nullptr;   // ev_acc: its last fold done
         DevBuf own_state, own_samples;
         DevBuf* state = nullptr;
         DevBuf* samples = nullptr;
@@ -929,8 +930,7 @@ struct ptg_context {
     Slot slot[kMaxSlots];
     uint32_t nslots = 1;
     uint32_t concurrency = 2;              // ptg_set_concurrency
-    hipStream_t acc_stream = nullptr;
-    hipEvent_t ev_render_start = nullptr, ev_acc_end = nullptr;
+    hipEvent_t ev_render_start = nullptr;
     ~ptg_context()
     {
         if(ev_main) (void)hipEventDestroy(ev_main);
@@ -946,22 +946,18 @@ struct ptg_context {
         }
         for(uint32_t k = 0; k < kMaxSlots; ++k)
         {
-            for(hipEvent_t e: {slot[k].ev_done, slot[k].ev_acc})
-                if(e) (void)hipEventDestroy(e);
+            if(slot[k].ev_acc) (void)hipEventDestroy(slot[k].ev_acc);
         }
-        for(hipEvent_t e: {ev_render_start, ev_acc_end})
-            if(e) (void)hipEventDestroy(e);
-        if(acc_stream) (void)hipStreamDestroy(acc_stream);
+        if(ev_render_start) (void)hipEventDestroy(ev_render_start);
         for(hipEvent_t e: ev_start) (void)hipEventDestroy(e);
         for(hipEvent_t e: ev_stop) (void)hipEventDestroy(e);
     }
 
     // Wait for everything queued on the context's streams: the caller's
-    // stream, the second streams, the extra chunk pipeline and the
-    // accumulation stream.
+    // stream, the second streams and the extra chunk pipeline.
     hipError_t drain() const
     {
-        for(hipStream_t st: {stream, side, acc_stream})
+        for(hipStream_t st: {stream, side})
             if(hipError_t e = hipStreamSynchronize(st)) return e;
         for(uint32_t k = 1; k < kMaxSlots; ++k)
             for(hipStream_t st: {slot[k].main, slot[k].side})
@@ -1164,7 +1160,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipEventRecord(ctx->ev_render_start, ctx->stream));
         for(uint32_t k = 1; k < nslots; ++k)
             PTG_HIP(hipStreamWaitEvent(slots[k].main, ctx->ev_render_start, 0));
-        PTG_HIP(hipStreamWaitEvent(ctx->acc_stream, ctx->ev_render_start, 0));
     }
     const DevScene sc = ctx->scene_args(cfg);
     // walk stack spill areas: one per (chunk pipeline, walk kind), since up to
@@ -1232,27 +1227,22 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
     }
     if(plan.empty())
         for(uint32_t j = j0, k = 0; j < j1; j += chunk, ++k) plan.push_back({j, std::min(chunk, j1 - j), k % nslots});
-    // Folds (k_accumulate, chunks in sample order on the accumulation stream)
-    // are issued lazily: a chunk's fold goes out just before the next chunk of
-    // its slot (which waits for it: it reuses the samples buffer), or at the
-    // end.  Issued right after its chunk, a fold's wait would sit in the
-    // accumulation stream ahead of the other slot's next launches, and HIP
-    // may map those two streams onto one hardware queue (GPU_MAX_HW_QUEUES 4):
-    // the other slot's first chunk then waited for this slot's whole chunk
-    // (profiles/r06c_timeline/).
-    std::vector<uint32_t> pending;
-    uint32_t last_of_slot[ptg_context::kMaxSlots];
-    for(uint32_t& v: last_of_slot) v = 0xFFFFFFFFu;
-    auto fold = [&](uint32_t k) -> int {
-        const Piece& pf = plan[k];
+    // Folds (k_accumulate: the chunks' samples into the running per-pixel
+    // sums, chunks in sample order) run on the chunk's own slot stream right
+    // after the chunk; a fold whose predecessor ran on the other slot first
+    // waits for that fold's event.  (A separate accumulation stream shared a
+    // hardware queue with slot 0's stream - HIP maps five streams onto
+    // GPU_MAX_HW_QUEUES = 4 queues - so a fold waiting for slot 1's chunk
+    // blocked slot 0's next launches behind it: profiles/r06c_timeline/.)
+    // A slot's next chunk then reuses its samples buffer after its fold in
+    // stream order, with no event at all.
+    uint32_t prev_slot = 0xFFFFFFFFu;
+    auto fold = [&](const Piece& pf) -> int {
         ptg_context::Slot& sl = slots[pf.slot];
         const int first = pf.j == j0, last = pf.j + pf.n >= j1;
-        hipStream_t as = sl.main;
-        if(nslots > 1)
-        {
-            as = ctx->acc_stream;
-            PTG_HIP(hipStreamWaitEvent(as, sl.ev_done, 0));
-        }
+        const hipStream_t as = sl.main;
+        if(nslots > 1 && prev_slot != 0xFFFFFFFFu && prev_slot != pf.slot)
+            PTG_HIP(hipStreamWaitEvent(as, slots[prev_slot].ev_acc, 0));
         if(int r = timed_begin(ctx, K_ACCUM, as)) return r;
         hipLaunchKernelGGL(k_accumulate, dim3(grid_for(pm.npix)), dim3(kBlock), 0, as, pm, pf.n,
                            sl.samples->as<float4>(), ctx->acc.as<float4>(), first, last, (float)cfg->samples_per_pixel,
@@ -1260,26 +1250,12 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         PTG_HIP(hipGetLastError());
         if(int r = timed_end(ctx, as)) return r;
         if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_acc, as));
-        return PTG_OK;
-    };
-    // issue the pending folds of chunks 0 .. upto - 1 of the plan, in order
-    auto flush_folds = [&](uint32_t upto) -> int {
-        size_t n = 0;
-        while(n < pending.size() && pending[n] < upto)
-        {
-            if(int r = fold(pending[n])) return r;
-            ++n;
-        }
-        pending.erase(pending.begin(), pending.begin() + n);
+        prev_slot = pf.slot;
         return PTG_OK;
     };
     for(const Piece& pc: plan)
     {
         const uint32_t j = pc.j, nj = pc.n, si = pc.slot;
-        if(last_of_slot[si] != 0xFFFFFFFFu)   // this slot's previous chunk is folded first (samples buffer)
-            if(int r = flush_folds(last_of_slot[si] + 1)) return r;
-        const bool slot_busy = last_of_slot[si] != 0xFFFFFFFFu;
-        last_of_slot[si] = uint32_t(&pc - plan.data());
         ptg_context::Slot& sl = slots[si];
         SlotState& sst = st[si];
         const DevScene sc_ext = walk_scene(si, 0), sc_sh = walk_scene(si, 1);
@@ -1290,8 +1266,6 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
         uint32_t* sky_list = sst.sky_list;
         uint32_t* counts = sst.counts;
         const hipStream_t ms = sl.main;
-        if(nslots > 1 && slot_busy)
-            PTG_HIP(hipStreamWaitEvent(ms, sl.ev_acc, 0));   // its samples buffer was folded in
         const size_t lanes = size_t((pm.npix + 7) / 8) * ((nj + 7) / 8) * 64;
         float4* out = sl.samples->as<float4>();
         if(!wf)
@@ -1409,19 +1383,10 @@ int render_map(ptg_context* ctx, const ptg_render_config* cfg, PixelMap pm, uint
                 PTG_HIP(hipStreamWaitEvent(ms, sl.ev_side, 0));
             }
         }
-        // the chunk's fold into the running per-pixel sums is issued later
-        // (fold below), in sample order
-        if(nslots > 1) PTG_HIP(hipEventRecord(sl.ev_done, ms));
-        pending.push_back(uint32_t(&pc - plan.data()));
-        if(nslots == 1)
-            if(int r = flush_folds(uint32_t(plan.size()))) return r;
+        if(int r = fold(pc)) return r;
     }
-    if(int r = flush_folds(uint32_t(plan.size()))) return r;
-    if(nslots > 1)
-    {   // the caller's stream sees the whole render
-        PTG_HIP(hipEventRecord(ctx->ev_acc_end, ctx->acc_stream));
-        PTG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_acc_end, 0));
-    }
+    if(nslots > 1 && prev_slot != 0xFFFFFFFFu && slots[prev_slot].main != ctx->stream)
+        PTG_HIP(hipStreamWaitEvent(ctx->stream, slots[prev_slot].ev_acc, 0));   // the caller's stream sees the whole render
 #if PTG_DEBUG
     {
         uint32_t dbg[kDebugSlots];
@@ -1566,12 +1531,9 @@ int ptg_context_create(int device, ptg_context** out)
     }
     for(uint32_t k = 0; k < kWfSlots; ++k)
     {
-        PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_done, hipEventDisableTiming));
         PTG_HIP(hipEventCreateWithFlags(&ctx->slot[k].ev_acc, hipEventDisableTiming));
     }
-    PTG_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
     PTG_HIP(hipEventCreateWithFlags(&ctx->ev_render_start, hipEventDisableTiming));
-    PTG_HIP(hipEventCreateWithFlags(&ctx->ev_acc_end, hipEventDisableTiming));
     ctx->nslots = kWfSlots;
     *out = ctx.release();
     return PTG_OK;
