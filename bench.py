@@ -579,9 +579,12 @@ def main():
         # pdf turns its sample, and so its pixel's sum, into NaN - in the
         # reference too (path_tracer.hh:735-737, main.cc:42)
         nan_px = int(np.isnan(acc_host[..., :3]).any(-1).sum())
-        return {"frame": f, "exact": got == want, "radiance": got["sha_radiance"] == want["sha_radiance"],
-                "bgra": got["sha_bgra"] == want["sha_bgra"], "nan_pixels": nan_px,
-                "golden": "tests/golden/full_render_s1024.json (the reference's strict build, whole image)"}
+        rad_ok, bgra_ok = got["sha_radiance"] == want["sha_radiance"], got["sha_bgra"] == want["sha_bgra"]
+        out = {"frame": f, "exact": rad_ok and bgra_ok, "radiance": rad_ok, "bgra": bgra_ok, "nan_pixels": nan_px}
+        if "nan_pixels_yx" in want:   # the strict build's NaN pixels (same places, same bits when exact)
+            out["nan_pixels_reference"] = len(want["nan_pixels_yx"])
+        return dict(out, **{
+                "golden": "tests/golden/full_render_s1024.json (the reference's strict build, whole image)"})
 
     def walk_levels(kind, workload, busy_ms, launches, iso_ms):
         """The roofline levels of one walk kind (extend / shadow) from the committed

@@ -35,5 +35,13 @@ def test_whole_frame_bit_identical_to_reference(gpu, assets_dir, frame):
     gpu.upload(s, include_static=True)
     bgra, acc = gpu.render(s.cfg, want_accum=True)
     gpu.synchronize()
-    got = image_hashes(acc.cpu().numpy(), bgra.cpu().numpy())
-    assert got == golden["frames"][str(frame)], "frame %d differs from the reference's whole image" % frame
+    acc_host = acc.cpu().numpy()
+    got = image_hashes(acc_host, bgra.cpu().numpy())
+    want = golden["frames"][str(frame)]
+    assert got == {k: want[k] for k in ("sha_radiance", "sha_bgra")}, "frame %d differs from the reference's whole image" % frame
+    # the NaN pixels (a path that met a zero BSDF pdf; the reference keeps
+    # them, path_tracer.hh:735-737): where the strict build has them
+    if "nan_pixels_yx" in want:
+        import numpy as np
+        nan_yx = np.argwhere(np.isnan(acc_host[..., :3]).any(-1)).tolist()
+        assert nan_yx == want["nan_pixels_yx"], (frame, nan_yx)
