@@ -87,3 +87,22 @@ def test_band_strict_vs_shipped(assets_dir, frame):
     assert max(st["T2_image_mean_rel_diff"]) < 5e-3
     assert st["T3_psnr_db"] >= 32.0
     assert st["T1_samples_within_1e-4"] > 0.5
+
+
+def test_shipped_band_fixture_matches_committed_rows():
+    """The fixture the GPU test recomputes against (make_shipped_band.py):
+    its strict-vs-shipped validator PSNR is the committed whole-frame row's,
+    and its arrays have the shapes the GPU test reads."""
+    import numpy as np
+    fx = json.load(open(os.path.join(GOLDEN, "shipped_band_s1024.json")))
+    arr = np.load(os.path.join(GOLDEN, "shipped_band_s1024.npz"))
+    rows = {(r["frame"], r["spp"]): r for r in json.load(open(os.path.join(GOLDEN, "parity_stats.json")))["metric_config"]["rows"]}
+    y0, y1 = fx["band_rows"]
+    for f in (0, 450):
+        st = fx["frames"][str(f)]
+        assert st["T3v_validator_good"] and max(st["band_mean_rel_diff"]) < 5e-3
+        if (f, 1024) in rows:
+            assert st["T3v_validator_psnr_db"] == rows[(f, 1024)]["T3v_validator_psnr_db"]
+        assert arr["shipped_half_f%d" % f].shape == (fx["height"] // 2, fx["width"] // 2, 3)
+        assert arr["shipped_band_f%d" % f].shape == (y1 - y0, fx["width"], 3)
+        assert arr["shipped_bgra_band_f%d" % f].shape == (y1 - y0, fx["width"], 4)
